@@ -1,0 +1,178 @@
+/*
+ * mpigx.h — C ABI of libmpigx, the MI355X-native collective engine that
+ * replaces libmpi for device-resident buffers under MPI.jl.
+ *
+ * Boundary: every MPI.jl collective on the hot path is one
+ * `ccall((:MPI_<Coll>, libmpi), Cint, ...)`.  Each entry point below takes the
+ * same arguments in the same order as the MPI function it replaces (count is
+ * a C int = Julia `Cint`, datatype/op are the MPICH handle values MPI.jl
+ * already passes as `Datatype(T).val` / `op.val`, deps/consts_mpich.jl:30-72),
+ * with the MPI_Comm replaced by an mpigx_comm_t.  Return values are MPI error
+ * classes (mpi.h:782-809) so MPI.jl's `@mpichk` (src/error.jl:5-8) wraps them
+ * unchanged.  Plain pointers and sizes only; no torch or HIP types.
+ *
+ * Semantics: blocking and collective, like MPI (results complete and visible
+ * to the host and the comm's stream on return), unless the communicator was
+ * switched to stream-ordered mode with mpigx_comm_set_blocking(comm, 0).
+ * Work is ordered after prior work on the comm's stream (default: the HIP
+ * null stream), which is how a caller's producer kernels are respected.
+ */
+#ifndef MPIGX_H
+#define MPIGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPIGX_VERSION_MAJOR 0
+#define MPIGX_VERSION_MINOR 1
+
+#define MPIGX_MAX_RANKS 16
+
+/* ---- error classes: identical to MPICH's (mpi.h:782-809) ---------------- */
+#define MPIGX_SUCCESS 0
+#define MPIGX_ERR_BUFFER 1
+#define MPIGX_ERR_COUNT 2
+#define MPIGX_ERR_TYPE 3
+#define MPIGX_ERR_COMM 5
+#define MPIGX_ERR_ROOT 7
+#define MPIGX_ERR_OP 9
+#define MPIGX_ERR_ARG 12
+#define MPIGX_ERR_OTHER 15
+#define MPIGX_ERR_INTERN 16
+#define MPIGX_ERR_NO_MEM 34
+
+/* ---- sentinels (deps/consts_mpich.jl:105) -------------------------------- */
+#define MPIGX_IN_PLACE ((void *)(intptr_t)-1)
+
+/* ---- datatypes: MPICH handle values (deps/consts_mpich.jl:47-72) --------- */
+#define MPIGX_CHAR 1275068673
+#define MPIGX_UNSIGNED_CHAR 1275068674
+#define MPIGX_BYTE 1275068685
+#define MPIGX_SHORT 1275068931
+#define MPIGX_UNSIGNED_SHORT 1275068932
+#define MPIGX_INT 1275069445
+#define MPIGX_UNSIGNED 1275069446
+#define MPIGX_LONG 1275070471
+#define MPIGX_UNSIGNED_LONG 1275070472
+#define MPIGX_FLOAT 1275069450
+#define MPIGX_DOUBLE 1275070475
+#define MPIGX_SIGNED_CHAR 1275068696
+#define MPIGX_WCHAR 1275069454
+#define MPIGX_INT8_T 1275068727
+#define MPIGX_INT16_T 1275068984
+#define MPIGX_INT32_T 1275069497
+#define MPIGX_INT64_T 1275070522
+#define MPIGX_UINT8_T 1275068731
+#define MPIGX_UINT16_T 1275068988
+#define MPIGX_UINT32_T 1275069501
+#define MPIGX_UINT64_T 1275070526
+#define MPIGX_C_FLOAT_COMPLEX 1275070528
+#define MPIGX_C_DOUBLE_COMPLEX 1275072577
+/* Extension: bf16 (no MPICH handle; MPI.jl maps BFloat16 to UINT16_T by size,
+ * datatypes.jl:281-284).  Encoded like an MPICH builtin of size 2 with an
+ * unused index.  Computed in fp32, RNE-rounded to bf16 after every op. */
+#define MPIGX_BFLOAT16 1275068912
+
+/* ---- ops: MPICH handle values (deps/consts_mpich.jl:30-45) --------------- */
+#define MPIGX_MAX 1476395009
+#define MPIGX_MIN 1476395010
+#define MPIGX_SUM 1476395011
+#define MPIGX_PROD 1476395012
+#define MPIGX_LAND 1476395013
+#define MPIGX_BAND 1476395014
+#define MPIGX_LOR 1476395015
+#define MPIGX_BOR 1476395016
+#define MPIGX_LXOR 1476395017
+#define MPIGX_BXOR 1476395018
+
+/* ---- reduction order (deterministic modes) ------------------------------- */
+/* MPICH: bit-exact with MPICH 3.3.2 on one node (binomial tree to rank 0 for
+ * <= 2 KiB or count < pof2, else Rabenseifner pre-step + recursive halving,
+ * including MIN/MAX operand roles).  LINEAR: rank-ordered left fold
+ * ((x0 op x1) op x2) ...  Both are deterministic and identical on all ranks. */
+#define MPIGX_ORDER_MPICH 0
+#define MPIGX_ORDER_LINEAR 1
+
+typedef struct mpigx_comm *mpigx_comm_t;
+typedef struct {
+    char internal[128];
+} mpigx_unique_id_t;
+
+/* ---- library ------------------------------------------------------------- */
+int mpigx_get_version(int *major, int *minor);
+/* MPI_Error_string analogue (src/error.jl:11-19). `len` in/out like MPI. */
+int mpigx_error_string(int errorcode, char *string, int *resultlen);
+/* Host-only validation of (datatype, op): MPIGX_SUCCESS, MPIGX_ERR_TYPE or
+ * MPIGX_ERR_OP following MPICH's op x type matrix.  Needs no GPU. */
+int mpigx_op_valid(int datatype, int op);
+/* MPI_Type_size analogue for the predefined types.  Needs no GPU. */
+int mpigx_type_size(int datatype, int *size);
+
+/* ---- communicator (src/comm.jl:6-115; rank -> GPU binding) -------------- */
+/* Rank 0 creates an id and distributes it out of band (host MPI_Bcast of
+ * 128 bytes, torch.distributed, a file ...); then every rank calls
+ * mpigx_comm_init_rank.  All ranks must be on one node. */
+int mpigx_get_unique_id(mpigx_unique_id_t *id);
+int mpigx_comm_init_rank(mpigx_comm_t *comm, int nranks, const mpigx_unique_id_t *id,
+                         int rank, int device);
+int mpigx_comm_free(mpigx_comm_t comm);
+int mpigx_comm_rank(mpigx_comm_t comm, int *rank);
+int mpigx_comm_size(mpigx_comm_t comm, int *size);
+int mpigx_comm_device(mpigx_comm_t comm, int *device);
+/* HIP stream (hipStream_t as void*) the comm's work is ordered on; NULL =
+ * the null stream. */
+int mpigx_comm_set_stream(mpigx_comm_t comm, void *stream);
+/* 1 (default): every call returns with results complete.  0: calls only
+ * enqueue on the stream (RCCL-like); mpigx_comm_synchronize reports errors. */
+int mpigx_comm_set_blocking(mpigx_comm_t comm, int blocking);
+int mpigx_comm_synchronize(mpigx_comm_t comm);
+int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
+
+/* ---- collectives (src/collective.jl ccall sites) ------------------------- */
+/* MPI_Barrier  — collective.jl:15-19 */
+int mpigx_barrier(mpigx_comm_t comm);
+/* MPI_Bcast    — collective.jl:29-37 */
+int mpigx_bcast(void *buffer, int count, int datatype, int root, mpigx_comm_t comm);
+/* MPI_Allgather — collective.jl:295-307 (sendbuf may be MPIGX_IN_PLACE) */
+int mpigx_allgather(const void *sendbuf, int sendcount, int sendtype, void *recvbuf,
+                    int recvcount, int recvtype, mpigx_comm_t comm);
+/* MPI_Alltoall — collective.jl:489-501 (sendbuf may be MPIGX_IN_PLACE) */
+int mpigx_alltoall(const void *sendbuf, int sendcount, int sendtype, void *recvbuf,
+                   int recvcount, int recvtype, mpigx_comm_t comm);
+/* MPI_Reduce   — collective.jl:605-618 (IN_PLACE at root; recvbuf ignored
+ * (may be NULL) elsewhere) */
+int mpigx_reduce(const void *sendbuf, void *recvbuf, int count, int datatype, int op,
+                 int root, mpigx_comm_t comm);
+/* MPI_Allreduce — collective.jl:691-701 (sendbuf may be MPIGX_IN_PLACE) */
+int mpigx_allreduce(const void *sendbuf, void *recvbuf, int count, int datatype, int op,
+                    mpigx_comm_t comm);
+/* MPI_Scan     — collective.jl:760-768 */
+int mpigx_scan(const void *sendbuf, void *recvbuf, int count, int datatype, int op,
+               mpigx_comm_t comm);
+/* MPI_Exscan   — collective.jl:834-842 (rank 0's recvbuf is left untouched) */
+int mpigx_exscan(const void *sendbuf, void *recvbuf, int count, int datatype, int op,
+                 mpigx_comm_t comm);
+
+/* ---- local ops (config 2; operators.jl built-in Op set on device) ------- */
+/* MPI_Reduce_local (mpi.h:1357): inoutbuf[i] = op(inoutbuf[i], inbuf[i]).
+ * Device pointers; blocking on the null stream. */
+int mpigx_reduce_local(const void *inbuf, void *inoutbuf, int count, int datatype, int op);
+/* out[i] = fold_{k<nin} in[k][i] in `order` (as if in[k] were rank k's
+ * buffer of an nin-rank Allreduce).  Device pointers; enqueued on `stream`
+ * (NULL = null stream), asynchronous.  nin in [1, MPIGX_MAX_RANKS]. */
+int mpigx_reduce_local_multi(const void *const *in, int nin, void *out, long long count,
+                             int datatype, int op, int order, void *stream);
+
+/* ---- device buffers (north-star subsystem 1: the ROCBuffer backing) ----- */
+int mpigx_malloc(void **ptr, size_t bytes);
+int mpigx_free(void *ptr);
+int mpigx_memcpy(void *dst, const void *src, size_t bytes); /* any direction, blocking */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPIGX_H */

@@ -1,0 +1,103 @@
+// common.hpp — definitions shared by the host runtime (mpigx.cpp) and the HIP
+// kernels (kern_*.hip): element representations, op codes, kernel argument
+// blocks.  The MPICH handle <-> representation mapping mirrors
+// deps/consts_mpich.jl:47-72 and src/datatypes.jl:29-60.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/mpigx.h"
+
+namespace mpigx {
+
+constexpr int kMaxRanks = MPIGX_MAX_RANKS;
+constexpr int kMaxBlocks = 1024;      // signal slots per rank per barrier
+constexpr int kThreads = 256;         // threads per block of every kernel
+
+// Element representations.  Several MPI handles share one (INT == INT32_T,
+// LONG == INT64_T, CHAR == SIGNED_CHAR == INT8_T, BYTE == UINT8_T ...).
+enum Rep : int {
+  R_I8 = 0, R_U8, R_I16, R_U16, R_I32, R_U32, R_I64, R_U64,
+  R_F32, R_F64, R_C64, R_C128, R_BF16, R_COUNT, R_NONE = -1
+};
+
+// Built-in ops (src/operators.jl:22-37), dense indices.
+enum OpCode : int {
+  O_SUM = 0, O_PROD, O_MIN, O_MAX, O_LAND, O_LOR, O_LXOR, O_BAND, O_BOR, O_BXOR, O_COUNT,
+  O_NONE = -1
+};
+
+// Fold schedule (template parameter of the fold kernels).
+enum Sched : int { S_TREE = 0, S_LINEAR = 1 };
+
+// What one fold-kernel launch does (runtime, uniform).
+enum FoldMode : int {
+  M_LOCAL = 0,        // out = fold(src[*]) over [0,count): config 2, no peers
+  M_AR_ONESHOT = 1,   // copy-in, barrier, every rank folds everything, barrier
+  M_AR_TWOSHOT = 2,   // copy-in, barrier, RS (own chunk), barrier, AG, barrier
+  M_RED_ONESHOT = 3,  // copy-in, barrier, root folds everything, barrier
+  M_RED_TWOSHOT = 4,  // copy-in, barrier, RS (own chunk), barrier, root gathers, barrier
+};
+
+// Copy-kernel modes (Bcast / Allgather / Alltoall / Barrier).
+enum CopyMode : int { C_BCAST = 0, C_ALLGATHER = 1, C_ALLTOALL = 2, C_BARRIER = 3 };
+
+// Per-call view of the communicator, passed by value to every kernel.
+struct PeerView {
+  int rank;
+  int n;
+  uint64_t epoch;              // first barrier epoch of this launch (monotone)
+  uint64_t timeout_ticks;      // wall_clock64 ticks (100 MHz) before giving up
+  uint64_t* sig[kMaxRanks];    // signal array [kMaxBlocks][kMaxRanks] of every rank
+  unsigned* err;               // host-visible error word (0 = ok)
+  char* stage[kMaxRanks];      // staging arena base of every rank (IPC-mapped)
+};
+
+// Fold-kernel arguments.  Sources/partition are resolved on the host.
+struct FoldArgs {
+  PeerView pv;
+  int mode;            // FoldMode
+  int esize;           // element size in bytes
+  long long count;     // elements in this launch (round)
+  long long gbase;     // element offset of this round in the whole message
+  long long chunk;     // elements per rank chunk (two-shot), multiple of vec
+  long long slice;     // elements per block slice, multiple of vec
+  // fold schedule
+  int ntree;           // active tree leaves (binomial: n; pre-step tree: pof2)
+  int rem;             // pre-step pairs (leaf s < rem folds src2[s] into src[s])
+  int owner_mode;      // 0: lower subtree is inout (binomial); 1: Rabenseifner owner roles
+  int pof2_log;        // log2(pof2) for owner computation
+  long long blk_len;   // Rabenseifner block length (count_total / pof2)
+  int root;            // reduce root (rank)
+  // leaf -> rank maps for collective modes (staging-sourced)
+  signed char leaf_rank[kMaxRanks];
+  signed char leaf2_rank[kMaxRanks];
+  // LOCAL mode sources / destinations (user pointers)
+  const void* src[kMaxRanks];
+  const void* src2[kMaxRanks];
+  const void* send;    // collective modes: my send buffer (may be == recv)
+  void* recv;          // output
+};
+
+struct CopyArgs {
+  PeerView pv;
+  int mode;            // CopyMode
+  int root;
+  long long bytes;     // bytes per rank contribution (bcast: whole buffer)
+  long long slice;     // bytes per block slice (multiple of 16)
+  long long total;     // alltoall: per-destination block stride in bytes (=bytes)
+  const void* send;
+  void* recv;
+};
+
+struct ScanArgs {
+  PeerView pv;
+  int exclusive;
+  int esize;
+  long long count;
+  long long slice;
+  const void* send;
+  void* recv;
+};
+
+}  // namespace mpigx

@@ -1,0 +1,194 @@
+// kernels.hpp — the three kernel families of libmpigx.
+//
+//  fold_kernel<OP,T,NMAX,SCHED>: local multi-buffer reduce (config 2) and the
+//      reducing collectives Allreduce! / Reduce! (src/collective.jl:605-714).
+//  scan_kernel<OP,T>: Scan! / Exscan! (collective.jl:760-857) with MPICH's
+//      recursive-doubling association and operand roles.
+//  copy_kernel: Bcast! / Allgather! / Alltoall! / Barrier (collective.jl:15-42,
+//      295-335, 489-532) — byte movement only.
+//
+// Data path of every collective (one launch per round, rounds bound the
+// staging arena): block b of every rank owns the same element slice(s);
+//   copy-in: my send slice(s) -> my staging arena (HBM, IPC-exported)
+//   barrier(b): the slices are visible to every peer
+//   compute: pull peer slices over xGMI (peer-mapped HBM), reduction fused
+//            into the pull, write the result to my recvbuf (and staging)
+//   barrier(b) ... final barrier(b): peers finished reading my staging.
+#pragma once
+#include "device.hpp"
+
+namespace mpigx {
+
+__device__ __forceinline__ long long lmin(long long a, long long b) { return a < b ? a : b; }
+
+template <class OP, class T, int NMAX, int SCHED>
+__global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
+  const T* const* src = reinterpret_cast<const T* const*>(A.src);
+  const T* const* src2 = reinterpret_cast<const T* const*>(A.src2);
+  const PeerView& pv = A.pv;
+  constexpr int W = VecW<T>::v;
+  const int b = blockIdx.x;
+  const long long tid = threadIdx.x, nt = blockDim.x;
+
+  if (A.mode == M_LOCAL) {
+    bool vec = ((uintptr_t)A.recv & 15) == 0;
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s)
+      if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
+#pragma unroll
+    for (int s = 0; s < NMAX / 2; ++s)
+      if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
+    // grid-stride over the whole range
+    const long long gtid = (long long)b * nt + tid, gnt = (long long)gridDim.x * nt;
+    fold_range<OP, T, NMAX, SCHED>(A, src, src2, 0, A.count, (T*)A.recv, nullptr, vec, gtid, gnt);
+    return;
+  }
+
+  T* recv = (T*)A.recv;
+  T* mine = (T*)pv.stage[pv.rank];
+  const char* send = (const char*)A.send;
+  const bool recv_vec = ((uintptr_t)recv & 15) == 0;
+  const int es = A.esize;
+  uint64_t ep = pv.epoch;
+
+  if (A.mode == M_AR_ONESHOT || A.mode == M_RED_ONESHOT) {
+    const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
+    block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);
+    if (!rank_barrier(pv, ep++)) return;
+    if (A.mode == M_AR_ONESHOT || pv.rank == A.root)
+      fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
+    rank_barrier(pv, ep++);
+    return;
+  }
+
+  // two-shot: chunk c = [c*chunk, (c+1)*chunk) ∩ [0,count), block b owns
+  // slice b of every chunk.
+  const int n = pv.n, r = pv.rank;
+  for (int c = 0; c < n; ++c) {
+    const long long c0 = lmin((long long)c * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+    block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);
+  }
+  if (!rank_barrier(pv, ep++)) return;
+  {
+    const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+    // reduce-scatter: my chunk from every rank's staging; result into my
+    // staging (for the peers' gather) and straight into my recvbuf.
+    const bool want_recv = (A.mode == M_AR_TWOSHOT) || (r == A.root);
+    if (want_recv)
+      fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, recv, mine, recv_vec, tid, nt);
+    else
+      fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, mine, nullptr, true, tid, nt);
+  }
+  (void)W;
+  if (!rank_barrier(pv, ep++)) return;
+  if (A.mode == M_AR_TWOSHOT || r == A.root) {
+    // allgather (or gather at root): every other rank's reduced chunk
+    for (int k = 1; k < n; ++k) {
+      const int p = (r + k) % n;  // stagger the peers so links load evenly
+      const long long c0 = lmin((long long)p * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+      const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+      const T* ps = (const T*)pv.stage[p];
+      block_copy((char*)(recv + lo), (const char*)(ps + lo), (hi - lo) * es);
+    }
+  }
+  rank_barrier(pv, ep++);
+}
+
+// ---------------------------------------------------------------------------
+// Scan / Exscan.  MPICH 3.3.2 MPIR_Scan/Exscan_intra_recursive_doubling: for
+// rank q and every set bit m of q, the block total of the m ranks just below
+// q's aligned 2m-block is folded in, in increasing m:
+//   scan:   rec = x_q; rec = OP(rec, T_m) ...
+//   exscan: ex  = T_m1; ex = OP(ex, T_m2) ...
+// T(block, owner) is computed as on rank `owner`: OP(inout = half holding the
+// owner, in = other half as computed on owner^half).
+// ---------------------------------------------------------------------------
+template <class OP, class T, int SIZE, int W>
+__device__ __forceinline__ void blk_total(const PeerView& pv, int base, int owner, long long e, T (&out)[W]) {
+  if constexpr (SIZE == 1) {
+    ld<T, W>(out, (const T*)pv.stage[base] + e);
+  } else {
+    constexpr int H = SIZE / 2;
+    const bool hi_own = (owner - base) & H;
+    T a[W], c[W];
+    blk_total<OP, T, H, W>(pv, base, hi_own ? owner ^ H : owner, e, a);       // low half
+    blk_total<OP, T, H, W>(pv, base + H, hi_own ? owner : owner ^ H, e, c);   // high half
+#pragma unroll
+    for (int w = 0; w < W; ++w) out[w] = hi_own ? OP::apply(c[w], a[w]) : OP::apply(a[w], c[w]);
+  }
+}
+
+template <class OP, class T, int W>
+__device__ __forceinline__ void blk_total_rt(const PeerView& pv, int m, int base, int owner, long long e, T (&out)[W]) {
+  switch (m) {
+    case 1: blk_total<OP, T, 1, W>(pv, base, owner, e, out); break;
+    case 2: blk_total<OP, T, 2, W>(pv, base, owner, e, out); break;
+    case 4: blk_total<OP, T, 4, W>(pv, base, owner, e, out); break;
+    default: blk_total<OP, T, 8, W>(pv, base, owner, e, out); break;
+  }
+}
+
+template <class OP, class T, int W>
+__device__ __forceinline__ void scan_at(const ScanArgs& A, long long e, T (&res)[W], bool& have) {
+  const int q = A.pv.rank;
+  have = !A.exclusive;
+  if (!A.exclusive) ld<T, W>(res, (const T*)A.pv.stage[q] + e);
+  for (int m = 1; m < A.pv.n; m <<= 1) {
+    if (!(q & m)) continue;
+    const int d = q ^ m;
+    T t[W];
+    blk_total_rt<OP, T, W>(A.pv, m, d & ~(m - 1), d, e, t);
+    if (!have) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) res[w] = t[w];
+      have = true;
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) res[w] = OP::apply(res[w], t[w]);
+    }
+  }
+}
+
+template <class OP, class T>
+__global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs A) {
+  constexpr int W = VecW<T>::v;
+  const PeerView& pv = A.pv;
+  const int b = blockIdx.x;
+  const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
+  T* mine = (T*)pv.stage[pv.rank];
+  block_copy((char*)(mine + lo), (const char*)A.send + lo * A.esize, (hi - lo) * A.esize);
+  uint64_t ep = pv.epoch;
+  if (!rank_barrier(pv, ep++)) return;
+  T* recv = (T*)A.recv;
+  const bool skip = A.exclusive && pv.rank == 0;  // rank 0's recvbuf untouched
+  if (!skip) {
+    const long long tid = threadIdx.x, nt = blockDim.x;
+    long long s = lo;
+    if (((uintptr_t)recv & 15) == 0) {
+      const long long nv = (hi - lo) / W;
+      for (long long i = tid; i < nv; i += nt) {
+        T r[W];
+        bool have;
+        scan_at<OP, T, W>(A, lo + i * W, r, have);
+        st<T, W>(recv + lo + i * W, r);
+      }
+      s = lo + nv * W;
+    }
+    for (long long e = s + tid; e < hi; e += nt) {
+      T r[1];
+      bool have;
+      scan_at<OP, T, 1>(A, e, r, have);
+      recv[e] = r[0];
+    }
+  }
+  rank_barrier(pv, ep++);
+}
+
+// ---------------------------------------------------------------------------
+// byte-movement collectives
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A);
+
+}  // namespace mpigx

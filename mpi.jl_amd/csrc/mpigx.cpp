@@ -1,0 +1,859 @@
+// mpigx.cpp — host runtime of libmpigx: the C ABI declared in include/mpigx.h.
+//
+// Replaces, for device-resident buffers, the libmpi that MPI.jl ccalls
+// (src/collective.jl ccall sites :17 :34 :304 :498 :615 :698 :765 :839).
+// Responsibilities:
+//   * MPICH handle -> element representation / op mapping and the MPICH
+//     op x type validity matrix (returns MPI_ERR_OP like MPICH);
+//   * communicator bootstrap (src/comm.jl rank -> GPU binding): a POSIX shm
+//     rendezvous keyed by a unique id exchanges hipIpc handles of every rank's
+//     staging arena (HBM) and signal array (uncached HBM);
+//   * per-call planning: MPICH-compatible fold schedule (binomial vs
+//     Rabenseifner regime, operand roles), one-shot vs two-shot algorithm,
+//     grid and slice sizes, rounds that bound the staging arena;
+//   * blocking MPI semantics on a HIP stream with device-side timeouts turned
+//     into MPI error classes.
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <mutex>
+#include <string>
+
+#include "common.hpp"
+#include "launch.hpp"
+
+using namespace mpigx;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// datatypes / ops (deps/consts_mpich.jl:30-72; src/datatypes.jl:29-60)
+// ---------------------------------------------------------------------------
+struct TypeInfo {
+  int handle;
+  Rep rep;
+  int size;
+  int kind;  // 0 int, 1 float, 2 complex, 3 byte (bitwise only), 4 none (copies only)
+};
+const TypeInfo kTypes[] = {
+    {MPIGX_INT8_T, R_I8, 1, 0},          {MPIGX_UINT8_T, R_U8, 1, 0},
+    {MPIGX_INT16_T, R_I16, 2, 0},        {MPIGX_UINT16_T, R_U16, 2, 0},
+    {MPIGX_INT32_T, R_I32, 4, 0},        {MPIGX_UINT32_T, R_U32, 4, 0},
+    {MPIGX_INT64_T, R_I64, 8, 0},        {MPIGX_UINT64_T, R_U64, 8, 0},
+    {MPIGX_BYTE, R_U8, 1, 3},            {MPIGX_SHORT, R_I16, 2, 0},
+    {MPIGX_UNSIGNED_SHORT, R_U16, 2, 0}, {MPIGX_INT, R_I32, 4, 0},
+    {MPIGX_UNSIGNED, R_U32, 4, 0},       {MPIGX_LONG, R_I64, 8, 0},
+    {MPIGX_UNSIGNED_LONG, R_U64, 8, 0},  {MPIGX_CHAR, R_I8, 1, 0},
+    {MPIGX_SIGNED_CHAR, R_I8, 1, 0},     {MPIGX_UNSIGNED_CHAR, R_U8, 1, 0},
+    {MPIGX_WCHAR, R_I32, 4, 4},          {MPIGX_FLOAT, R_F32, 4, 1},
+    {MPIGX_DOUBLE, R_F64, 8, 1},         {MPIGX_C_FLOAT_COMPLEX, R_C64, 8, 2},
+    {MPIGX_C_DOUBLE_COMPLEX, R_C128, 16, 2},
+    {MPIGX_BFLOAT16, R_BF16, 2, 1},
+};
+
+const TypeInfo* find_type(int h) {
+  for (const auto& t : kTypes)
+    if (t.handle == h) return &t;
+  return nullptr;
+}
+
+int op_code(int h) {
+  switch (h) {
+    case MPIGX_SUM: return O_SUM;
+    case MPIGX_PROD: return O_PROD;
+    case MPIGX_MIN: return O_MIN;
+    case MPIGX_MAX: return O_MAX;
+    case MPIGX_LAND: return O_LAND;
+    case MPIGX_LOR: return O_LOR;
+    case MPIGX_LXOR: return O_LXOR;
+    case MPIGX_BAND: return O_BAND;
+    case MPIGX_BOR: return O_BOR;
+    case MPIGX_BXOR: return O_BXOR;
+    default: return O_NONE;
+  }
+}
+
+// MPICH 3.3.2 op x type matrix (probed with MPI_Reduce_local, pinned in
+// tests/golden/op_type_matrix.json).
+int validate(int dtype, int op, const TypeInfo** ti, int* oc) {
+  const TypeInfo* t = find_type(dtype);
+  if (!t) return MPIGX_ERR_TYPE;
+  const int o = op_code(op);
+  if (o == O_NONE) return MPIGX_ERR_OP;
+  bool ok = false;
+  switch (t->kind) {
+    case 0: ok = true; break;
+    case 1: ok = !(o == O_BAND || o == O_BOR || o == O_BXOR); break;
+    case 2: ok = (o == O_SUM || o == O_PROD); break;
+    case 3: ok = (o == O_BAND || o == O_BOR || o == O_BXOR); break;
+    default: ok = false;
+  }
+  if (!ok) return MPIGX_ERR_OP;
+  if (ti) *ti = t;
+  if (oc) *oc = o;
+  return MPIGX_SUCCESS;
+}
+
+FoldLauncher fold_launcher(Rep r) {
+  switch (r) {
+    case R_I8: return launch_fold_i8;
+    case R_U8: return launch_fold_u8;
+    case R_I16: return launch_fold_i16;
+    case R_U16: return launch_fold_u16;
+    case R_I32: return launch_fold_i32;
+    case R_U32: return launch_fold_u32;
+    case R_I64: return launch_fold_i64;
+    case R_U64: return launch_fold_u64;
+    case R_F32: return launch_fold_f32;
+    case R_F64: return launch_fold_f64;
+    case R_C64: return launch_fold_c64;
+    case R_C128: return launch_fold_c128;
+    case R_BF16: return launch_fold_bf16;
+    default: return nullptr;
+  }
+}
+ScanLauncher scan_launcher(Rep r) {
+  switch (r) {
+    case R_I8: return launch_scan_i8;
+    case R_U8: return launch_scan_u8;
+    case R_I16: return launch_scan_i16;
+    case R_U16: return launch_scan_u16;
+    case R_I32: return launch_scan_i32;
+    case R_U32: return launch_scan_u32;
+    case R_I64: return launch_scan_i64;
+    case R_U64: return launch_scan_u64;
+    case R_F32: return launch_scan_f32;
+    case R_F64: return launch_scan_f64;
+    case R_C64: return launch_scan_c64;
+    case R_C128: return launch_scan_c128;
+    case R_BF16: return launch_scan_bf16;
+    default: return nullptr;
+  }
+}
+
+long long env_ll(const char* name, long long dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return strtoll(v, nullptr, 0);
+}
+
+int pof2_of(int n) {
+  int p = 1;
+  while (p * 2 <= n) p *= 2;
+  return p;
+}
+int log2i(int p) {
+  int l = 0;
+  while ((1 << l) < p) ++l;
+  return l;
+}
+long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
+long long rup(long long a, long long b) { return cdiv(a, b) * b; }
+
+// ---------------------------------------------------------------------------
+// shm rendezvous
+// ---------------------------------------------------------------------------
+constexpr uint64_t kMagic = 0x6d70696778763031ull;  // "mpigxv01"
+
+struct ShmRank {
+  int pid;
+  int device;
+  int pci_bus;
+  int pci_dev;
+  unsigned long long stage_bytes;
+  unsigned long long stage_ptr;  // raw pointer (same-process peers)
+  unsigned long long sig_ptr;
+  hipIpcMemHandle_t stage_h;
+  hipIpcMemHandle_t sig_h;
+};
+struct ShmBlock {
+  std::atomic<uint64_t> magic;
+  int nranks;
+  std::atomic<int> arrived;
+  std::atomic<int> connected;
+  std::atomic<int> failed;
+  ShmRank ranks[kMaxRanks];
+};
+
+// Unique id payload (fits in mpigx_unique_id_t::internal).
+struct IdPayload {
+  char name[64];
+  uint64_t magic;
+};
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// communicator
+// ---------------------------------------------------------------------------
+struct mpigx_comm {
+  int rank = 0, n = 1, device = 0;
+  hipStream_t stream = nullptr;
+  int blocking = 1;
+  int order = MPIGX_ORDER_MPICH;
+  bool broken = false;
+  uint64_t epoch = 1;
+  uint64_t timeout_ticks = 0;
+  // local resources
+  char* stage = nullptr;
+  size_t stage_bytes = 0;
+  uint64_t* sig = nullptr;
+  unsigned* err = nullptr;  // host-pinned, device-written
+  // peers (index = rank; self included)
+  char* peer_stage[kMaxRanks] = {};
+  uint64_t* peer_sig[kMaxRanks] = {};
+  bool peer_opened[kMaxRanks] = {};
+  ShmBlock* shm = nullptr;
+  // tuning
+  int max_blocks = 256;
+  long long oneshot_max = 256 << 10;
+  long long bytes_per_block = 64 << 10;
+  std::mutex mu;
+};
+
+namespace {
+
+#define HIPCK(x)                                                                   \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "[mpigx] %s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      return MPIGX_ERR_INTERN;                                                     \
+    }                                                                              \
+  } while (0)
+
+PeerView make_view(mpigx_comm* c) {
+  PeerView pv;
+  memset(&pv, 0, sizeof pv);
+  pv.rank = c->rank;
+  pv.n = c->n;
+  pv.epoch = c->epoch;
+  pv.timeout_ticks = c->timeout_ticks;
+  pv.err = c->err;
+  for (int p = 0; p < c->n; ++p) {
+    pv.sig[p] = c->peer_sig[p];
+    pv.stage[p] = c->peer_stage[p];
+  }
+  return pv;
+}
+
+// After enqueueing: in blocking mode wait and translate device errors.
+int finish(mpigx_comm* c) {
+  if (!c->blocking) return MPIGX_SUCCESS;
+  HIPCK(hipStreamSynchronize(c->stream));
+  if (__atomic_load_n(c->err, __ATOMIC_ACQUIRE) != 0) {
+    c->broken = true;
+    return MPIGX_ERR_OTHER;
+  }
+  return MPIGX_SUCCESS;
+}
+
+int grid_for(mpigx_comm* c, long long bytes) {
+  long long g = cdiv(bytes, c->bytes_per_block);
+  if (g < 1) g = 1;
+  if (g > c->max_blocks) g = c->max_blocks;
+  return (int)g;
+}
+
+// Fold schedule for an n-leaf reduction (MPICH single-node semantics):
+//   small (count*size <= 2048 or count < pof2): binomial tree over relative
+//   ranks (rel = (rank - root) mod n), lower subtree = inout;
+//   large: Rabenseifner — odd rank 2i+1 folds 2i (pre-step, inout = odd),
+//   then the pairwise tree over newranks with owner-based operand roles.
+// `ptrs[k]` is what leaf k reads for rank k (staging base or user pointer).
+void plan_schedule(mpigx_comm* c, FoldArgs& a, int n, int root, long long count_total, int esize,
+                   const void* const* ptrs, int* nmax, int* sched, int order) {
+  a.rem = 0;
+  a.owner_mode = 0;
+  a.pof2_log = 0;
+  a.blk_len = 1;
+  (void)c;
+  if (order == MPIGX_ORDER_LINEAR) {
+    *sched = S_LINEAR;
+    *nmax = 16;
+    a.ntree = n;
+    for (int k = 0; k < n; ++k) a.src[k] = ptrs[k];
+    return;
+  }
+  *sched = S_TREE;
+  const int pof2 = pof2_of(n);
+  if (count_total * esize <= 2048 || count_total < pof2) {
+    a.ntree = n;
+    for (int k = 0; k < n; ++k) a.src[k] = ptrs[(k + root) % n];
+    *nmax = n <= 8 ? 8 : 16;
+  } else {
+    const int rem = n - pof2;
+    a.ntree = pof2;
+    a.rem = rem;
+    for (int s = 0; s < pof2; ++s) {
+      if (s < rem) {
+        a.src[s] = ptrs[2 * s + 1];
+        a.src2[s] = ptrs[2 * s];
+      } else {
+        a.src[s] = ptrs[s + rem];
+      }
+    }
+    a.owner_mode = 1;
+    a.pof2_log = log2i(pof2);
+    a.blk_len = count_total / pof2;
+    *nmax = pof2 <= 8 ? 8 : 16;
+  }
+}
+
+// Shared driver for Allreduce / Reduce.
+int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, const TypeInfo* t,
+                  int oc, int root, bool all) {
+  const int n = c->n, es = t->size;
+  const int vec = es >= 16 ? 1 : 16 / es;
+  FoldLauncher L = fold_launcher(t->rep);
+  // elements per round: staging holds a whole round
+  long long round = (long long)(c->stage_bytes / es);
+  round = (round / (n * (long long)vec)) * n * vec;
+  const char* algo_env = getenv("MPIGX_ALGO");
+  for (long long off = 0; off < count; off += round) {
+    const long long cnt = count - off < round ? count - off : round;
+    FoldArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.esize = es;
+    a.count = cnt;
+    a.gbase = off;
+    a.root = root;
+    a.send = (const char*)send + off * es;
+    a.recv = recv ? (char*)recv + off * es : nullptr;
+    int nmax, sched;
+    const void* ptrs[kMaxRanks];
+    for (int p = 0; p < n; ++p) ptrs[p] = c->peer_stage[p];
+    plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
+    bool oneshot = cnt * es <= c->oneshot_max;
+    if (algo_env && !strcmp(algo_env, "oneshot")) oneshot = true;
+    if (algo_env && !strcmp(algo_env, "twoshot")) oneshot = false;
+    int grid, nbar;
+    if (oneshot) {
+      a.mode = all ? M_AR_ONESHOT : M_RED_ONESHOT;
+      grid = grid_for(c, cnt * es);
+      a.slice = rup(cdiv(cnt, grid), vec);
+      nbar = 2;
+    } else {
+      a.mode = all ? M_AR_TWOSHOT : M_RED_TWOSHOT;
+      a.chunk = rup(cdiv(cnt, n), vec);
+      grid = grid_for(c, a.chunk * es);
+      a.slice = rup(cdiv(a.chunk, grid), vec);
+      nbar = 3;
+    }
+    HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
+    c->epoch += nbar;
+  }
+  return finish(c);
+}
+
+int check_comm(mpigx_comm* c) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (c->broken) return MPIGX_ERR_OTHER;
+  if (hipSetDevice(c->device) != hipSuccess) return MPIGX_ERR_INTERN;
+  return MPIGX_SUCCESS;
+}
+
+int copy_n1(mpigx_comm* c, void* dst, const void* src, size_t bytes) {
+  if (dst != src && bytes) HIPCK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+  return finish(c);
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int mpigx_get_version(int* major, int* minor) {
+  if (major) *major = MPIGX_VERSION_MAJOR;
+  if (minor) *minor = MPIGX_VERSION_MINOR;
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_error_string(int code, char* str, int* len) {
+  const char* s;
+  switch (code) {
+    case MPIGX_SUCCESS: s = "No MPI error"; break;
+    case MPIGX_ERR_BUFFER: s = "Invalid buffer pointer"; break;
+    case MPIGX_ERR_COUNT: s = "Invalid count argument"; break;
+    case MPIGX_ERR_TYPE: s = "Invalid datatype argument"; break;
+    case MPIGX_ERR_COMM: s = "Invalid communicator"; break;
+    case MPIGX_ERR_ROOT: s = "Invalid root"; break;
+    case MPIGX_ERR_OP: s = "Invalid MPI_Op (not defined for this datatype)"; break;
+    case MPIGX_ERR_ARG: s = "Invalid argument"; break;
+    case MPIGX_ERR_OTHER: s = "Other MPI error (mpigx: peer did not arrive / communicator broken)"; break;
+    case MPIGX_ERR_INTERN: s = "Internal MPI error (mpigx: HIP runtime failure)"; break;
+    case MPIGX_ERR_NO_MEM: s = "Out of memory"; break;
+    default: s = "Unknown error"; break;
+  }
+  if (str) {
+    strncpy(str, s, 511);
+    str[511] = 0;
+  }
+  if (len) *len = (int)strlen(s);
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_op_valid(int datatype, int op) { return validate(datatype, op, nullptr, nullptr); }
+
+int mpigx_type_size(int datatype, int* size) {
+  const TypeInfo* t = find_type(datatype);
+  if (!t) return MPIGX_ERR_TYPE;
+  if (size) *size = t->size;
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_get_unique_id(mpigx_unique_id_t* id) {
+  if (!id) return MPIGX_ERR_ARG;
+  memset(id, 0, sizeof *id);
+  IdPayload p;
+  memset(&p, 0, sizeof p);
+  unsigned long long r = 0;
+  FILE* f = fopen("/dev/urandom", "rb");
+  if (f) {
+    if (fread(&r, sizeof r, 1, f) != 1) r = 0;
+    fclose(f);
+  }
+  r ^= (unsigned long long)getpid() << 32 ^ (unsigned long long)(now_s() * 1e9);
+  snprintf(p.name, sizeof p.name, "/mpigx-%d-%016llx", (int)getpid(), r);
+  p.magic = kMagic;
+  memcpy(id->internal, &p, sizeof p);
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t* id, int rank, int device) {
+  if (!out || !id) return MPIGX_ERR_ARG;
+  if (nranks < 1 || nranks > kMaxRanks) return MPIGX_ERR_ARG;
+  if (rank < 0 || rank >= nranks) return MPIGX_ERR_ARG;
+  IdPayload p;
+  memcpy(&p, id->internal, sizeof p);
+  if (p.magic != kMagic) return MPIGX_ERR_ARG;
+  HIPCK(hipSetDevice(device));
+
+  mpigx_comm* c = new mpigx_comm();
+  c->rank = rank;
+  c->n = nranks;
+  c->device = device;
+  c->max_blocks = (int)env_ll("MPIGX_MAX_BLOCKS", 256);
+  if (c->max_blocks < 1) c->max_blocks = 1;
+  if (c->max_blocks > kMaxBlocks) c->max_blocks = kMaxBlocks;
+  c->oneshot_max = env_ll("MPIGX_ONESHOT_MAX", 256 << 10);
+  c->bytes_per_block = env_ll("MPIGX_BYTES_PER_BLOCK", 64 << 10);
+  c->stage_bytes = (size_t)env_ll("MPIGX_STAGING_BYTES", 512ll << 20);
+  c->stage_bytes = (c->stage_bytes + 4095) & ~(size_t)4095;
+  c->timeout_ticks = (uint64_t)(env_ll("MPIGX_TIMEOUT_MS", 60000) * 100000ll);  // 100 MHz clock
+
+  HIPCK(hipMalloc(&c->stage, c->stage_bytes));
+  const size_t sig_bytes = (size_t)kMaxBlocks * kMaxRanks * sizeof(uint64_t);
+  HIPCK(hipExtMallocWithFlags((void**)&c->sig, sig_bytes, hipDeviceMallocUncached));
+  HIPCK(hipMemset(c->sig, 0, sig_bytes));
+  HIPCK(hipHostMalloc((void**)&c->err, 64, hipHostMallocCoherent | hipHostMallocMapped));
+  memset(c->err, 0, 64);
+  HIPCK(hipDeviceSynchronize());
+  c->peer_stage[rank] = c->stage;
+  c->peer_sig[rank] = c->sig;
+
+  if (nranks > 1) {
+    // rendezvous
+    const double t0 = now_s();
+    const double limit = env_ll("MPIGX_INIT_TIMEOUT_MS", 120000) / 1000.0;
+    int fd = -1;
+    if (rank == 0) {
+      fd = shm_open(p.name, O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0 || ftruncate(fd, sizeof(ShmBlock)) != 0) {
+        fprintf(stderr, "[mpigx] shm_open(%s): %s\n", p.name, strerror(errno));
+        return MPIGX_ERR_INTERN;
+      }
+    } else {
+      while ((fd = shm_open(p.name, O_RDWR, 0600)) < 0) {
+        if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
+        usleep(1000);
+      }
+      struct stat st;
+      while (fstat(fd, &st) == 0 && (size_t)st.st_size < sizeof(ShmBlock)) {
+        if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
+        usleep(1000);
+      }
+    }
+    void* m = mmap(nullptr, sizeof(ShmBlock), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return MPIGX_ERR_INTERN;
+    c->shm = (ShmBlock*)m;
+    if (rank == 0) {
+      c->shm->nranks = nranks;
+      c->shm->magic.store(kMagic, std::memory_order_release);
+    } else {
+      while (c->shm->magic.load(std::memory_order_acquire) != kMagic) {
+        if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
+        usleep(1000);
+      }
+      if (c->shm->nranks != nranks) return MPIGX_ERR_ARG;
+    }
+    ShmRank& me = c->shm->ranks[rank];
+    me.pid = getpid();
+    me.device = device;
+    hipDeviceProp_t prop;
+    HIPCK(hipGetDeviceProperties(&prop, device));
+    me.pci_bus = prop.pciBusID;
+    me.pci_dev = prop.pciDeviceID;
+    me.stage_bytes = c->stage_bytes;
+    me.stage_ptr = (unsigned long long)(uintptr_t)c->stage;
+    me.sig_ptr = (unsigned long long)(uintptr_t)c->sig;
+    HIPCK(hipIpcGetMemHandle(&me.stage_h, c->stage));
+    HIPCK(hipIpcGetMemHandle(&me.sig_h, c->sig));
+    c->shm->arrived.fetch_add(1, std::memory_order_acq_rel);
+    while (c->shm->arrived.load(std::memory_order_acquire) < nranks) {
+      if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
+      usleep(200);
+    }
+    for (int q = 0; q < nranks; ++q) {
+      if (q == rank) continue;
+      const ShmRank& pr = c->shm->ranks[q];
+      if (pr.stage_bytes != c->stage_bytes) return MPIGX_ERR_ARG;  // MPIGX_STAGING_BYTES must agree
+      if (pr.pid == me.pid) {
+        c->peer_stage[q] = (char*)(uintptr_t)pr.stage_ptr;
+        c->peer_sig[q] = (uint64_t*)(uintptr_t)pr.sig_ptr;
+      } else {
+        void* ps = nullptr;
+        void* pg = nullptr;
+        HIPCK(hipIpcOpenMemHandle(&ps, pr.stage_h, hipIpcMemLazyEnablePeerAccess));
+        HIPCK(hipIpcOpenMemHandle(&pg, pr.sig_h, hipIpcMemLazyEnablePeerAccess));
+        c->peer_stage[q] = (char*)ps;
+        c->peer_sig[q] = (uint64_t*)pg;
+        c->peer_opened[q] = true;
+      }
+    }
+    c->shm->connected.fetch_add(1, std::memory_order_acq_rel);
+    while (c->shm->connected.load(std::memory_order_acquire) < nranks) {
+      if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
+      usleep(200);
+    }
+    if (rank == 0) shm_unlink(p.name);  // every rank has it mapped now
+  }
+  *out = c;
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_comm_free(mpigx_comm_t c) {
+  if (!c) return MPIGX_ERR_COMM;
+  (void)hipSetDevice(c->device);
+  int rc = MPIGX_SUCCESS;
+  if (c->n > 1 && !c->broken) {
+    // make sure no peer still reads our staging
+    const int b = c->blocking;
+    c->blocking = 1;
+    rc = mpigx_barrier(c);
+    c->blocking = b;
+  }
+  (void)hipStreamSynchronize(c->stream);
+  for (int q = 0; q < c->n; ++q) {
+    if (!c->peer_opened[q]) continue;
+    (void)hipIpcCloseMemHandle(c->peer_stage[q]);
+    (void)hipIpcCloseMemHandle(c->peer_sig[q]);
+  }
+  if (c->shm) munmap(c->shm, sizeof(ShmBlock));
+  (void)hipFree(c->stage);
+  (void)hipFree(c->sig);
+  (void)hipHostFree(c->err);
+  delete c;
+  return rc;
+}
+
+int mpigx_comm_rank(mpigx_comm_t c, int* rank) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (rank) *rank = c->rank;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_size(mpigx_comm_t c, int* size) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (size) *size = c->n;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_device(mpigx_comm_t c, int* device) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (device) *device = c->device;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_set_stream(mpigx_comm_t c, void* stream) {
+  if (!c) return MPIGX_ERR_COMM;
+  c->stream = (hipStream_t)stream;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_set_blocking(mpigx_comm_t c, int blocking) {
+  if (!c) return MPIGX_ERR_COMM;
+  c->blocking = blocking ? 1 : 0;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_synchronize(mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const int b = c->blocking;
+  c->blocking = 1;
+  rc = finish(c);
+  c->blocking = b;
+  return rc;
+}
+int mpigx_comm_set_reduce_order(mpigx_comm_t c, int order) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (order != MPIGX_ORDER_MPICH && order != MPIGX_ORDER_LINEAR) return MPIGX_ERR_ARG;
+  c->order = order;
+  return MPIGX_SUCCESS;
+}
+
+// ---------------------------------------------------------------------------
+int mpigx_barrier(mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  if (c->n == 1) return finish(c);
+  CopyArgs a;
+  memset(&a, 0, sizeof a);
+  a.pv = make_view(c);
+  a.mode = C_BARRIER;
+  HIPCK(launch_copy(dim3(1), c->stream, a));
+  c->epoch += 1;
+  return finish(c);
+}
+
+int mpigx_bcast(void* buf, int count, int datatype, int root, mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const TypeInfo* t = find_type(datatype);
+  if (!t) return MPIGX_ERR_TYPE;
+  if (count < 0) return MPIGX_ERR_COUNT;
+  if (root < 0 || root >= c->n) return MPIGX_ERR_ROOT;
+  if (count == 0) return MPIGX_SUCCESS;
+  if (!buf) return MPIGX_ERR_BUFFER;
+  if (c->n == 1) return finish(c);
+  const long long bytes = (long long)count * t->size;
+  const long long round = (long long)(c->stage_bytes & ~(size_t)15);
+  for (long long off = 0; off < bytes; off += round) {
+    const long long len = bytes - off < round ? bytes - off : round;
+    CopyArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.mode = C_BCAST;
+    a.root = root;
+    a.bytes = len;
+    const int g = grid_for(c, len);
+    a.slice = rup(cdiv(len, g), 16);
+    a.send = (const char*)buf + off;
+    a.recv = (char*)buf + off;
+    HIPCK(launch_copy(dim3(g), c->stream, a));
+    c->epoch += 2;
+  }
+  return finish(c);
+}
+
+static int gather_like(const void* send, int scount, int stype, void* recv, int rcount, int rtype,
+                       mpigx_comm_t c, bool alltoall) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const TypeInfo* rt = find_type(rtype);
+  if (!rt) return MPIGX_ERR_TYPE;
+  if (rcount < 0) return MPIGX_ERR_COUNT;
+  const bool inplace = send == MPIGX_IN_PLACE;
+  if (!inplace) {
+    const TypeInfo* st = find_type(stype);
+    if (!st) return MPIGX_ERR_TYPE;
+    if (scount < 0) return MPIGX_ERR_COUNT;
+    if ((long long)scount * st->size != (long long)rcount * rt->size) return MPIGX_ERR_ARG;
+  }
+  const long long bytes = (long long)rcount * rt->size;  // per rank block
+  if (bytes == 0) return MPIGX_SUCCESS;
+  if (!recv || (!inplace && !send)) return MPIGX_ERR_BUFFER;
+  const int n = c->n, r = c->rank;
+  const char* s = inplace ? (alltoall ? (const char*)recv : (const char*)recv + (long long)r * bytes)
+                          : (const char*)send;
+  if (n == 1) return copy_n1(c, alltoall ? recv : (char*)recv, s, bytes);
+  // rounds: allgather stages `bytes` per rank; alltoall stages n*round
+  const long long cap = alltoall ? (long long)(c->stage_bytes / n) & ~15ll : (long long)c->stage_bytes & ~15ll;
+  for (long long off = 0; off < bytes; off += cap) {
+    const long long len = bytes - off < cap ? bytes - off : cap;
+    CopyArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.mode = alltoall ? C_ALLTOALL : C_ALLGATHER;
+    a.bytes = len;
+    a.total = bytes;
+    const int g = grid_for(c, len * (alltoall ? n : 1));
+    a.slice = rup(cdiv(len, g), 16);
+    if (alltoall) {
+      a.send = s + off;
+      a.recv = (char*)recv + off;
+      // staging layout for the round: block p at p*len
+    } else {
+      a.send = s + off;
+      a.recv = (char*)recv + off;
+    }
+    HIPCK(launch_copy(dim3(g), c->stream, a));
+    c->epoch += 2;
+  }
+  return finish(c);
+}
+
+int mpigx_allgather(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
+                    mpigx_comm_t c) {
+  return gather_like(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, c, false);
+}
+int mpigx_alltoall(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
+                   mpigx_comm_t c) {
+  return gather_like(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, c, true);
+}
+
+int mpigx_allreduce(const void* sendbuf, void* recvbuf, int count, int datatype, int op, mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const TypeInfo* t;
+  int oc;
+  if ((rc = validate(datatype, op, &t, &oc))) return rc;
+  if (count < 0) return MPIGX_ERR_COUNT;
+  if (count == 0) return MPIGX_SUCCESS;
+  if (!recvbuf || !sendbuf) return MPIGX_ERR_BUFFER;
+  const void* s = sendbuf == MPIGX_IN_PLACE ? recvbuf : sendbuf;
+  if (c->n == 1) return copy_n1(c, recvbuf, s, (size_t)count * t->size);
+  return reduce_common(c, s, recvbuf, count, t, oc, 0, true);
+}
+
+int mpigx_reduce(const void* sendbuf, void* recvbuf, int count, int datatype, int op, int root, mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const TypeInfo* t;
+  int oc;
+  if ((rc = validate(datatype, op, &t, &oc))) return rc;
+  if (count < 0) return MPIGX_ERR_COUNT;
+  if (root < 0 || root >= c->n) return MPIGX_ERR_ROOT;
+  if (count == 0) return MPIGX_SUCCESS;
+  const bool isroot = c->rank == root;
+  if (isroot && !recvbuf) return MPIGX_ERR_BUFFER;
+  if (!sendbuf || (sendbuf == MPIGX_IN_PLACE && !isroot)) return MPIGX_ERR_BUFFER;
+  const void* s = sendbuf == MPIGX_IN_PLACE ? recvbuf : sendbuf;
+  if (c->n == 1) return copy_n1(c, recvbuf, s, (size_t)count * t->size);
+  return reduce_common(c, s, isroot ? recvbuf : nullptr, count, t, oc, root, false);
+}
+
+static int scan_common(const void* sendbuf, void* recvbuf, int count, int datatype, int op, mpigx_comm_t c,
+                       int exclusive) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const TypeInfo* t;
+  int oc;
+  if ((rc = validate(datatype, op, &t, &oc))) return rc;
+  if (count < 0) return MPIGX_ERR_COUNT;
+  if (count == 0) return MPIGX_SUCCESS;
+  if (!recvbuf || !sendbuf) return MPIGX_ERR_BUFFER;
+  const void* s = sendbuf == MPIGX_IN_PLACE ? recvbuf : sendbuf;
+  const int es = t->size;
+  if (c->n == 1) {
+    if (exclusive) return finish(c);
+    return copy_n1(c, recvbuf, s, (size_t)count * es);
+  }
+  ScanLauncher L = scan_launcher(t->rep);
+  const int vec = es >= 16 ? 1 : 16 / es;
+  long long round = (long long)(c->stage_bytes / es) / vec * vec;
+  for (long long off = 0; off < count; off += round) {
+    const long long cnt = count - off < round ? count - off : round;
+    ScanArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.exclusive = exclusive;
+    a.esize = es;
+    a.count = cnt;
+    const int g = grid_for(c, cnt * es);
+    a.slice = rup(cdiv(cnt, g), vec);
+    a.send = (const char*)s + off * es;
+    a.recv = (char*)recvbuf + off * es;
+    HIPCK(L(oc, dim3(g), c->stream, a));
+    c->epoch += 2;
+  }
+  return finish(c);
+}
+
+int mpigx_scan(const void* sendbuf, void* recvbuf, int count, int datatype, int op, mpigx_comm_t c) {
+  return scan_common(sendbuf, recvbuf, count, datatype, op, c, 0);
+}
+int mpigx_exscan(const void* sendbuf, void* recvbuf, int count, int datatype, int op, mpigx_comm_t c) {
+  return scan_common(sendbuf, recvbuf, count, datatype, op, c, 1);
+}
+
+// ---------------------------------------------------------------------------
+// local ops
+// ---------------------------------------------------------------------------
+int mpigx_reduce_local_multi(const void* const* in, int nin, void* out, long long count, int datatype, int op,
+                             int order, void* stream) {
+  const TypeInfo* t;
+  int oc;
+  int rc = validate(datatype, op, &t, &oc);
+  if (rc) return rc;
+  if (nin < 1 || nin > kMaxRanks) return MPIGX_ERR_ARG;
+  if (order != MPIGX_ORDER_MPICH && order != MPIGX_ORDER_LINEAR) return MPIGX_ERR_ARG;
+  if (count < 0) return MPIGX_ERR_COUNT;
+  if (count == 0) return MPIGX_SUCCESS;
+  if (!in || !out) return MPIGX_ERR_BUFFER;
+  for (int k = 0; k < nin; ++k)
+    if (!in[k]) return MPIGX_ERR_BUFFER;
+  FoldArgs a;
+  memset(&a, 0, sizeof a);
+  a.mode = M_LOCAL;
+  a.esize = t->size;
+  a.count = count;
+  a.recv = out;
+  int nmax, sched;
+  plan_schedule(nullptr, a, nin, 0, count, t->size, in, &nmax, &sched, order);
+  // grid: enough 256-thread blocks to cover the range once, capped so each
+  // thread strides a few times (memory-bound: ~8 waves/SIMD resident)
+  const int vec = t->size >= 16 ? 1 : 16 / t->size;
+  long long g = cdiv(cdiv(count, vec), kThreads);
+  const long long cap = env_ll("MPIGX_LOCAL_MAX_BLOCKS", 4096);
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  FoldLauncher L = fold_launcher(t->rep);
+  hipError_t e = L(oc, nmax, sched, dim3((unsigned)g), (hipStream_t)stream, a);
+  if (e != hipSuccess) {
+    fprintf(stderr, "[mpigx] reduce_local_multi launch: %s\n", hipGetErrorString(e));
+    return MPIGX_ERR_INTERN;
+  }
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_reduce_local(const void* inbuf, void* inoutbuf, int count, int datatype, int op) {
+  if (count < 0) return MPIGX_ERR_COUNT;
+  const void* ptrs[2] = {inoutbuf, inbuf};  // leaf 0 = inout (lower subtree), leaf 1 = in
+  int rc = mpigx_reduce_local_multi(ptrs, 2, inoutbuf, count, datatype, op, MPIGX_ORDER_LINEAR, nullptr);
+  if (rc) return rc;
+  HIPCK(hipStreamSynchronize(nullptr));
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_malloc(void** ptr, size_t bytes) {
+  if (!ptr) return MPIGX_ERR_ARG;
+  if (hipMalloc(ptr, bytes ? bytes : 1) != hipSuccess) return MPIGX_ERR_NO_MEM;
+  return MPIGX_SUCCESS;
+}
+int mpigx_free(void* ptr) {
+  if (ptr && hipFree(ptr) != hipSuccess) return MPIGX_ERR_INTERN;
+  return MPIGX_SUCCESS;
+}
+int mpigx_memcpy(void* dst, const void* src, size_t bytes) {
+  if (!bytes) return MPIGX_SUCCESS;
+  HIPCK(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+  return MPIGX_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,20 @@
+"""mpigx — MI355X-native collective engine behind MPI.jl's collective API.
+
+`import mpigx as MPI` gives the MPI.jl names (Init, COMM_WORLD, Comm_rank,
+Allreduce_ (= Allreduce!), Reduce_, Bcast_, Allgather_, Alltoall_, Scan_,
+Exscan_, SUM/MAX/..., Op, Datatype, Buffer, IN_PLACE, MPIError) over
+libmpigx.so for device-resident (ROCm) buffers.
+"""
+from . import consts
+from ._lib import HEADER_PATH, LIB_PATH, lib
+from .api import *  # noqa: F401,F403
+from .api import (COMM_WORLD, IN_PLACE, Barrier, Buffer, Comm, Datatype, MPIError, Op, error_string,
+                  reduce_local_multi)
+
+
+def __getattr__(name):
+    # COMM_WORLD is rebound by Init(); expose the live value
+    if name == "COMM_WORLD":
+        from . import api
+        return api.COMM_WORLD
+    raise AttributeError(name)

@@ -1,0 +1,72 @@
+"""ctypes binding of libmpigx.so (include/mpigx.h).
+
+The library is built in-tree (mpi.jl_amd/lib/libmpigx.so, see
+mpi.jl_amd/csrc/Makefile).  There is no fallback: if the shared object is
+missing, loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MPIGX_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmpigx.so"))
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "mpigx.h")
+
+_lib = None
+
+c_int, c_void_p, c_longlong, c_size_t = ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_size_t
+
+
+class UniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+# name -> (restype, argtypes)
+PROTOTYPES = {
+    "mpigx_get_version": (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "mpigx_error_string": (c_int, [c_int, ctypes.c_char_p, ctypes.POINTER(c_int)]),
+    "mpigx_op_valid": (c_int, [c_int, c_int]),
+    "mpigx_type_size": (c_int, [c_int, ctypes.POINTER(c_int)]),
+    "mpigx_get_unique_id": (c_int, [ctypes.POINTER(UniqueId)]),
+    "mpigx_comm_init_rank": (c_int, [ctypes.POINTER(c_void_p), c_int, ctypes.POINTER(UniqueId), c_int, c_int]),
+    "mpigx_comm_free": (c_int, [c_void_p]),
+    "mpigx_comm_rank": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
+    "mpigx_comm_size": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
+    "mpigx_comm_device": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
+    "mpigx_comm_set_stream": (c_int, [c_void_p, c_void_p]),
+    "mpigx_comm_set_blocking": (c_int, [c_void_p, c_int]),
+    "mpigx_comm_synchronize": (c_int, [c_void_p]),
+    "mpigx_comm_set_reduce_order": (c_int, [c_void_p, c_int]),
+    "mpigx_barrier": (c_int, [c_void_p]),
+    "mpigx_bcast": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mpigx_allgather": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "mpigx_alltoall": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "mpigx_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "mpigx_allreduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mpigx_scan": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mpigx_exscan": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mpigx_reduce_local": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int]),
+    "mpigx_reduce_local_multi": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_longlong, c_int, c_int, c_int,
+                                         c_void_p]),
+    "mpigx_malloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),
+    "mpigx_free": (c_int, [c_void_p]),
+    "mpigx_memcpy": (c_int, [c_void_p, c_void_p, c_size_t]),
+}
+
+
+def lib():
+    """Load libmpigx.so (once).  Raises if the HIP extension was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libmpigx.so not found at {LIB_PATH}: build it with `make -C mpi.jl_amd/csrc` "
+                "(or __graft_entry__.build()); mpigx has no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in PROTOTYPES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib

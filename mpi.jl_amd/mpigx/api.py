@@ -1,0 +1,716 @@
+"""MPI.jl's collective API surface, over libmpigx, for device-resident buffers.
+
+This is the host-side mirror of the reference's plugin point: Julia is absent
+from this image, so the MPI.jl wrappers that north_star keeps (src/comm.jl,
+src/buffers.jl, src/datatypes.jl, src/operators.jl, src/collective.jl) are
+restated here in Python with the same names (`!` becomes a trailing `_`),
+the same argument meaning, defaults and error behaviour:
+
+* argument checks are the reference's `@assert_minlength` /`@assert`
+  (buffers.jl:25-31) and raise ``AssertionError``;
+* non-zero return codes raise :class:`MPIError` like ``@mpichk``
+  (error.jl:5-8);
+* IN_PLACE, ``nothing``-recvbuf on non-roots, count defaults and the
+  allocating/scalar forms follow collective.jl line by line (cited per
+  function).
+
+Device buffers are torch tensors on a ROCm device (the ``ROCBuffer`` role of
+SURVEY.md §7 step 7); the bytes never leave HBM.  The Julia ccall glue that
+does the same for MPI.jl is mpi.jl_amd/julia/MPIGX.jl.
+"""
+from __future__ import annotations
+
+import ctypes
+import operator
+import os
+import time
+
+from . import consts as C
+from ._lib import UniqueId, lib
+
+IN_PLACE = object()  # MPI_IN_PLACE sentinel (consts_mpich.jl:105)
+_IN_PLACE_PTR = ctypes.c_void_p(-1 & ((1 << 64) - 1))
+
+
+class MPIError(Exception):
+    """error.jl:1-19: an MPI error code with its error string."""
+
+    def __init__(self, code: int):
+        self.code = code
+        super().__init__(f"MPIError({code}): {error_string(code)}")
+
+
+def error_string(code: int) -> str:
+    buf = ctypes.create_string_buffer(512)
+    n = ctypes.c_int(0)
+    lib().mpigx_error_string(code, buf, ctypes.byref(n))
+    return buf.value.decode()
+
+
+def _check(rc: int):
+    if rc != C.MPI_SUCCESS:
+        raise MPIError(rc)
+
+
+# ---------------------------------------------------------------------------
+# Datatype (src/datatypes.jl:16-60, 269-292)
+# ---------------------------------------------------------------------------
+class Datatype:
+    __slots__ = ("val", "name")
+
+    def __init__(self, T, name=None):
+        if isinstance(T, Datatype):
+            self.val, self.name = T.val, T.name
+            return
+        if isinstance(T, int) and name is not None:
+            self.val, self.name = T, name
+            return
+        dt = _datatype_of(T)
+        self.val, self.name = dt.val, dt.name
+
+    def __eq__(self, o):
+        return isinstance(o, Datatype) and o.val == self.val
+
+    def __hash__(self):
+        return hash(self.val)
+
+    def __repr__(self):
+        return f"MPI.Datatype({self.name})"
+
+
+def _mk(name, val):
+    return Datatype(val, name)
+
+
+INT8_T, UINT8_T = _mk("INT8_T", C.MPI_INT8_T), _mk("UINT8_T", C.MPI_UINT8_T)
+INT16_T, UINT16_T = _mk("INT16_T", C.MPI_INT16_T), _mk("UINT16_T", C.MPI_UINT16_T)
+INT32_T, UINT32_T = _mk("INT32_T", C.MPI_INT32_T), _mk("UINT32_T", C.MPI_UINT32_T)
+INT64_T, UINT64_T = _mk("INT64_T", C.MPI_INT64_T), _mk("UINT64_T", C.MPI_UINT64_T)
+BYTE, CHAR, WCHAR = _mk("BYTE", C.MPI_BYTE), _mk("CHAR", C.MPI_CHAR), _mk("WCHAR", C.MPI_WCHAR)
+FLOAT, DOUBLE = _mk("FLOAT", C.MPI_FLOAT), _mk("DOUBLE", C.MPI_DOUBLE)
+C_FLOAT_COMPLEX, C_DOUBLE_COMPLEX = _mk("C_FLOAT_COMPLEX", C.MPI_C_FLOAT_COMPLEX), _mk(
+    "C_DOUBLE_COMPLEX", C.MPI_C_DOUBLE_COMPLEX)
+BFLOAT16 = _mk("BFLOAT16", C.MPIGX_BFLOAT16)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _datatype_of(T) -> Datatype:
+    """Datatype(T) for torch dtypes / Python scalar types (datatypes.jl:29-60).
+
+    Unnamed 1/2/4/8-byte primitives go by size to UINT8/16/32/64_T exactly as
+    datatypes.jl:281-284 does (so float16 and bool are integer bit patterns,
+    as in the reference); bfloat16 gets mpigx's BFLOAT16 extension.
+    """
+    torch = _torch()
+    table = {
+        torch.int8: INT8_T, torch.uint8: UINT8_T, torch.int16: INT16_T, torch.int32: INT32_T,
+        torch.int64: INT64_T, torch.float32: FLOAT, torch.float64: DOUBLE,
+        torch.complex64: C_FLOAT_COMPLEX, torch.complex128: C_DOUBLE_COMPLEX,
+        torch.bfloat16: BFLOAT16, torch.float16: UINT16_T, torch.bool: UINT8_T,
+    }
+    for nm, dt in (("uint16", UINT16_T), ("uint32", UINT32_T), ("uint64", UINT64_T)):
+        if hasattr(torch, nm):
+            table[getattr(torch, nm)] = dt
+    if T in table:
+        return table[T]
+    if T is int:
+        return INT64_T
+    if T is float:
+        return DOUBLE
+    if T is complex:
+        return C_DOUBLE_COMPLEX
+    if T is bool:
+        return UINT8_T
+    raise TypeError(f"no MPI datatype for {T!r}")
+
+
+_INTEGER = ("int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64")
+_FLOAT = ("float32", "float64", "bfloat16")
+_COMPLEX = ("complex64", "complex128")
+
+
+def _kind(T) -> str:
+    name = str(T).replace("torch.", "")
+    if T is int or name in _INTEGER:
+        return "int"
+    if T is float or name in _FLOAT:
+        return "float"
+    if T is complex or name in _COMPLEX:
+        return "complex"
+    return "other"
+
+
+# ---------------------------------------------------------------------------
+# Op (src/operators.jl)
+# ---------------------------------------------------------------------------
+class Op:
+    """Built-in op handle, or a user function (OpWrapper, operators.jl:56-88)."""
+    __slots__ = ("val", "name", "fn", "iscommutative")
+
+    def __init__(self, f, T=None, iscommutative=False, *, _val=None, _name=None):
+        if _val is not None:
+            self.val, self.name, self.fn, self.iscommutative = _val, _name, None, True
+            return
+        if isinstance(f, Op):
+            self.val, self.name, self.fn, self.iscommutative = f.val, f.name, f.fn, f.iscommutative
+            return
+        b = _builtin_for(f, T)
+        if b is not None:
+            self.val, self.name, self.fn, self.iscommutative = b.val, b.name, None, True
+        else:
+            # user-defined: inout[i] = f(in[i], inout[i]) (operators.jl:60-69)
+            self.val, self.name, self.fn, self.iscommutative = None, getattr(f, "__name__", "user"), f, iscommutative
+
+    def __repr__(self):
+        return f"MPI.Op({self.name})"
+
+
+def _op(name, val):
+    return Op(None, _val=val, _name=name)
+
+
+OP_NULL = _op("OP_NULL", C.MPI_OP_NULL)
+BAND, BOR, BXOR = _op("BAND", C.MPI_BAND), _op("BOR", C.MPI_BOR), _op("BXOR", C.MPI_BXOR)
+LAND, LOR, LXOR = _op("LAND", C.MPI_LAND), _op("LOR", C.MPI_LOR), _op("LXOR", C.MPI_LXOR)
+MAX, MIN = _op("MAX", C.MPI_MAX), _op("MIN", C.MPI_MIN)
+PROD, SUM = _op("PROD", C.MPI_PROD), _op("SUM", C.MPI_SUM)
+REPLACE, NO_OP = _op("REPLACE", C.MPI_REPLACE), _op("NO_OP", C.MPI_NO_OP)
+
+
+def _builtin_for(f, T):
+    """operators.jl:39-45: min/max/+/* for numbers, &,|,xor for integers."""
+    k = _kind(T) if T is not None else "any"
+    num = k in ("int", "float", "any")
+    if f is min and num:
+        return MIN
+    if f is max and num:
+        return MAX
+    if f is operator.add and (num or k == "complex"):
+        return SUM
+    if f is operator.mul and (num or k == "complex"):
+        return PROD
+    if k in ("int", "any"):
+        if f is operator.and_:
+            return BAND
+        if f is operator.or_:
+            return BOR
+        if f is operator.xor:
+            return BXOR
+    return None
+
+
+def _as_op(op, T) -> Op:
+    if isinstance(op, Op):
+        return op
+    return Op(op, T)
+
+
+# ---------------------------------------------------------------------------
+# Buffer (src/buffers.jl:78-127)
+# ---------------------------------------------------------------------------
+class Buffer:
+    """MPI.Buffer(data, count, datatype): device tensor + count + Datatype."""
+    __slots__ = ("data", "count", "datatype")
+
+    def __init__(self, data, count=None, datatype=None):
+        if isinstance(data, Buffer):
+            self.data, self.count, self.datatype = data.data, data.count, data.datatype
+            return
+        self.data = data
+        self.count = int(count if count is not None else data.numel())
+        self.datatype = Datatype(datatype if datatype is not None else data.dtype)
+
+
+def _ptr(buf):
+    if buf is None:
+        return None
+    if buf is IN_PLACE:
+        return _IN_PLACE_PTR
+    if isinstance(buf, Buffer):
+        buf = buf.data
+    if not getattr(buf, "is_cuda", False):
+        raise TypeError("mpigx handles device-resident buffers (ROCm tensors); host buffers stay on libmpi")
+    if not buf.is_contiguous():
+        raise ValueError("non-contiguous device buffers need derived datatypes (SURVEY.md §8f, out of scope)")
+    return ctypes.c_void_p(buf.data_ptr())
+
+
+def _len(buf):
+    if isinstance(buf, Buffer):
+        return buf.count
+    return buf.numel()
+
+
+def _eltype(buf):
+    if isinstance(buf, Buffer):
+        return buf.datatype
+    return Datatype(buf.dtype)
+
+
+def _assert_minlength(buf, count):
+    """buffers.jl:25-31: only array buffers are checked."""
+    if buf is not None and buf is not IN_PLACE:
+        assert _len(buf) >= count, f"buffer length {_len(buf)} < count {count}"
+
+
+def _is_array(x):
+    return hasattr(x, "numel") or isinstance(x, Buffer)
+
+
+# ---------------------------------------------------------------------------
+# Comm (src/comm.jl) + environment (src/environment.jl)
+# ---------------------------------------------------------------------------
+class Comm:
+    __slots__ = ("val", "_rank", "_size", "device")
+
+    def __init__(self, handle, rank, size, device):
+        self.val, self._rank, self._size, self.device = handle, rank, size, device
+
+    def __repr__(self):
+        return f"MPI.Comm(rank={self._rank}, size={self._size}, device={self.device})"
+
+
+COMM_WORLD = None
+_state = {"init": False, "final": False, "pg_owned": False}
+
+
+def _env_int(*names, default=None):
+    for n in names:
+        v = os.environ.get(n)
+        if v not in (None, ""):
+            return int(v)
+    return default
+
+
+def _bootstrap_id(rank, size):
+    """Distribute rank 0's mpigx unique id (the role MPI_Bcast plays for the
+    Julia glue)."""
+    uid = UniqueId()
+    if rank == 0:
+        _check(lib().mpigx_get_unique_id(ctypes.byref(uid)))
+    if size == 1:
+        return uid
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", rank=rank, world_size=size)
+        _state["pg_owned"] = True
+    obj = [bytes(uid.internal) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    ctypes.memmove(uid.internal, obj[0], 128)
+    return uid
+
+
+def Init(threadlevel=None):
+    """environment.jl:80: Init binds this rank to its GPU and builds COMM_WORLD.
+
+    Rank/size come from the launcher (torchrun RANK/WORLD_SIZE/LOCAL_RANK or
+    hydra PMI_RANK/PMI_SIZE/MPI_LOCALRANKID); device = MPIGX_DEVICE or
+    local_rank mod visible devices (comm.jl:107 Comm_split_type(SHARED)).
+    """
+    global COMM_WORLD
+    if _state["init"]:
+        raise AssertionError("MPI.Init called twice")
+    torch = _torch()
+    rank = _env_int("RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", default=0)
+    size = _env_int("WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", default=1)
+    local = _env_int("LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", default=rank)
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise RuntimeError("mpigx: no ROCm device visible")
+    device = _env_int("MPIGX_DEVICE", default=local % ndev)
+    torch.cuda.set_device(device)
+    uid = _bootstrap_id(rank, size)
+    h = ctypes.c_void_p()
+    _check(lib().mpigx_comm_init_rank(ctypes.byref(h), size, ctypes.byref(uid), rank, device))
+    COMM_WORLD = Comm(h, rank, size, device)
+    _state["init"] = True
+    return COMM_WORLD
+
+
+def Initialized():
+    return _state["init"]
+
+
+def Finalized():
+    return _state["final"]
+
+
+def Finalize():
+    global COMM_WORLD
+    if COMM_WORLD is not None:
+        _check(lib().mpigx_comm_free(COMM_WORLD.val))
+        COMM_WORLD = None
+    if _state["pg_owned"]:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+        _state["pg_owned"] = False
+    _state["final"] = True
+
+
+def Wtime():
+    return time.perf_counter()
+
+
+def has_rocm():
+    """has_cuda() analogue (environment.jl:308-323): device buffers supported."""
+    try:
+        lib()
+        return _torch().cuda.is_available()
+    except Exception:
+        return False
+
+
+def Comm_rank(comm: Comm) -> int:
+    return comm._rank
+
+
+def Comm_size(comm: Comm) -> int:
+    return comm._size
+
+
+def Comm_dup(comm: Comm) -> Comm:
+    """comm.jl:78: a new communicator over the same ranks (own arenas/epochs).
+
+    Its unique id is broadcast over `comm` itself, through the device engine.
+    """
+    torch = _torch()
+    uid = UniqueId()
+    if comm._rank == 0:
+        _check(lib().mpigx_get_unique_id(ctypes.byref(uid)))
+    t = torch.frombuffer(bytearray(uid.internal), dtype=torch.uint8).to(f"cuda:{comm.device}")
+    Bcast_(t, 0, comm)
+    ctypes.memmove(uid.internal, bytes(t.cpu().numpy().tobytes()), 128)
+    h = ctypes.c_void_p()
+    _check(lib().mpigx_comm_init_rank(ctypes.byref(h), comm._size, ctypes.byref(uid), comm._rank, comm.device))
+    return Comm(h, comm._rank, comm._size, comm.device)
+
+
+def Comm_split_type(comm: Comm, split_type, key, info=None) -> Comm:
+    """comm.jl:107: COMM_TYPE_SHARED on one node is every rank."""
+    if split_type != C.MPI_COMM_TYPE_SHARED:
+        raise MPIError(C.MPI_ERR_ARG)
+    return Comm_dup(comm)
+
+
+def free(comm: Comm):
+    if comm is not None and comm.val:
+        _check(lib().mpigx_comm_free(comm.val))
+        comm.val = None
+
+
+def set_reduce_order(comm: Comm, order: int):
+    """mpigx extension: MPIGX_ORDER_MPICH (default) or MPIGX_ORDER_LINEAR."""
+    _check(lib().mpigx_comm_set_reduce_order(comm.val, order))
+
+
+def _stream(comm):
+    torch = _torch()
+    s = torch.cuda.current_stream(comm.device).cuda_stream
+    lib().mpigx_comm_set_stream(comm.val, ctypes.c_void_p(s))
+
+
+# ---------------------------------------------------------------------------
+# collectives (src/collective.jl)
+# ---------------------------------------------------------------------------
+def Barrier(comm: Comm):
+    """collective.jl:15-19."""
+    _stream(comm)
+    _check(lib().mpigx_barrier(comm.val))
+
+
+def Bcast_(buf, *args):
+    """Bcast!(buf[, count], root, comm) — collective.jl:29-42."""
+    if len(args) == 3:
+        count, root, comm = args
+    else:
+        root, comm = args
+        count = _len(buf)
+    _stream(comm)
+    _check(lib().mpigx_bcast(_ptr(buf), int(count), _eltype(buf).val, int(root), comm.val))
+    return buf
+
+
+def Allgather_(*args):
+    """Allgather!(sendbuf, recvbuf, count, comm) / Allgather!(sendrecvbuf, count, comm)
+    — collective.jl:295-311."""
+    if len(args) == 3:
+        sendbuf, (recvbuf, count, comm) = IN_PLACE, args
+    else:
+        sendbuf, recvbuf, count, comm = args
+    assert recvbuf is not None
+    _assert_minlength(recvbuf, count * Comm_size(comm))
+    _assert_minlength(sendbuf, count)
+    T = _eltype(recvbuf)
+    _stream(comm)
+    _check(lib().mpigx_allgather(_ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val, comm.val))
+    return recvbuf
+
+
+def Allgather(*args):
+    """Allgather(sendbuf[, count], comm) / Allgather(obj, comm) — collective.jl:327-335."""
+    torch = _torch()
+    if len(args) == 3:
+        sendbuf, count, comm = args
+        return Allgather_(sendbuf, torch.empty(Comm_size(comm) * count, dtype=sendbuf.dtype,
+                                               device=sendbuf.device), count, comm)
+    sendbuf, comm = args
+    if _is_array(sendbuf):
+        return Allgather(sendbuf, _len(sendbuf), comm)
+    ref = _scalar_ref(sendbuf, comm)
+    out = torch.empty(Comm_size(comm), dtype=ref.dtype, device=ref.device)
+    Allgather_(ref, out, 1, comm)
+    return out.cpu().tolist()
+
+
+def Alltoall_(*args):
+    """Alltoall!(sendbuf, recvbuf, count, comm) — collective.jl:489-501.
+    The in-place 3-argument form (:503-505 references an undefined `recvbuf`
+    in the reference) is implemented as evidently intended."""
+    if len(args) == 3:
+        sendbuf, (recvbuf, count, comm) = IN_PLACE, args
+    else:
+        sendbuf, recvbuf, count, comm = args
+    buflength = count * Comm_size(comm)
+    _assert_minlength(recvbuf, buflength)
+    _assert_minlength(sendbuf, buflength)
+    if sendbuf is not IN_PLACE:
+        assert _eltype(sendbuf) == _eltype(recvbuf)
+    T = _eltype(recvbuf)
+    _stream(comm)
+    _check(lib().mpigx_alltoall(_ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val, comm.val))
+    return recvbuf
+
+
+def Alltoall(sendbuf, count, comm):
+    """collective.jl:529-532."""
+    torch = _torch()
+    recvbuf = torch.empty(Comm_size(comm) * count, dtype=sendbuf.dtype, device=sendbuf.device)
+    return Alltoall_(sendbuf, recvbuf, count, comm)
+
+
+def _scalar_ref(obj, comm):
+    """`Ref(object)` of the scalar forms, as a 1-element device tensor."""
+    torch = _torch()
+    if isinstance(obj, bool):
+        dt = torch.uint8
+    elif isinstance(obj, int):
+        dt = torch.int64
+    elif isinstance(obj, float):
+        dt = torch.float64
+    elif isinstance(obj, complex):
+        dt = torch.complex128
+    elif hasattr(obj, "dtype") and hasattr(obj, "item"):
+        dt = obj.dtype
+        obj = obj.item()
+    else:
+        raise TypeError(f"unsupported scalar {obj!r}")
+    return torch.tensor([obj], dtype=dt, device=f"cuda:{comm.device}")
+
+
+def _user_fold(xs, fn):
+    """OpWrapper semantics (operators.jl:60-69): inout = f(in, inout), with the
+    lower rank as `in`; rank-ordered, so associativity suffices."""
+    acc = xs[0]
+    for x in xs[1:]:
+        acc = fn(acc, x)
+    return acc
+
+
+def _user_collective(kind, sendbuf, recvbuf, count, op, root, comm):
+    """Non-builtin Op on device buffers: gather the operands with the engine's
+    Allgather, fold with the user function as device tensor ops."""
+    torch = _torch()
+    n, r = Comm_size(comm), Comm_rank(comm)
+    src = recvbuf if sendbuf is IN_PLACE else sendbuf
+    flat = src.reshape(-1)[:count].contiguous()
+    g = torch.empty(n * count, dtype=flat.dtype, device=flat.device)
+    Allgather_(flat, g, count, comm)
+    xs = list(g.view(n, count).unbind(0))
+    if kind in ("allreduce", "reduce"):
+        if kind == "reduce" and r != root:
+            return recvbuf
+        res = _user_fold(xs, op.fn)
+    elif kind == "scan":
+        res = _user_fold(xs[: r + 1], op.fn)
+    else:  # exscan
+        if r == 0:
+            return recvbuf
+        res = _user_fold(xs[:r], op.fn)
+    recvbuf.reshape(-1)[:count].copy_(res.to(recvbuf.dtype))
+    return recvbuf
+
+
+def Reduce_(*args):
+    """Reduce!(sendbuf, recvbuf, count, op, root, comm)          collective.jl:605
+    Reduce!(sendbuf, recvbuf, op, root, comm)                     :626
+    Reduce!(buf, op, root, comm)  (IN_PLACE at root)              :632"""
+    if len(args) == 4:
+        buf, op, root, comm = args
+        if Comm_rank(comm) == root:
+            return Reduce_(IN_PLACE, buf, _len(buf), op, root, comm)
+        return Reduce_(buf, None, _len(buf), op, root, comm)
+    if len(args) == 5:
+        sendbuf, recvbuf, op, root, comm = args
+        return Reduce_(sendbuf, recvbuf, _len(sendbuf), op, root, comm)
+    sendbuf, recvbuf, count, op, root, comm = args
+    isroot = Comm_rank(comm) == root
+    _assert_minlength(sendbuf, count)
+    if isroot:
+        assert recvbuf is not None
+        _assert_minlength(recvbuf, count)
+    T = _eltype(recvbuf) if sendbuf is IN_PLACE else _eltype(sendbuf)
+    opx = _as_op(op, _torch_dtype(sendbuf if sendbuf is not IN_PLACE else recvbuf))
+    if opx.val is None:
+        return _user_collective("reduce", sendbuf, recvbuf, count, opx, root, comm)
+    _stream(comm)
+    _check(lib().mpigx_reduce(_ptr(sendbuf), _ptr(recvbuf), int(count), T.val, opx.val, int(root), comm.val))
+    return recvbuf
+
+
+def Reduce(sendbuf, op, root, comm):
+    """collective.jl:657-666: allocating; `nothing` (None) on non-roots."""
+    torch = _torch()
+    if _is_array(sendbuf):
+        recv = torch.empty_like(sendbuf) if Comm_rank(comm) == root else None
+        return Reduce_(sendbuf, recv, _len(sendbuf), op, root, comm)
+    ref = _scalar_ref(sendbuf, comm)
+    if Comm_rank(comm) == root:
+        out = torch.empty_like(ref)
+        Reduce_(ref, out, 1, op, root, comm)
+        return out.item()
+    Reduce_(ref, None, 1, op, root, comm)
+    return None
+
+
+def _torch_dtype(buf):
+    if isinstance(buf, Buffer):
+        buf = buf.data
+    return getattr(buf, "dtype", None)
+
+
+def Allreduce_(*args):
+    """Allreduce!(sendbuf, recvbuf, count, op, comm)   collective.jl:691-701
+    Allreduce!(sendbuf, recvbuf, op, comm)              :707 (count = length(recvbuf))
+    Allreduce!(buf, op, comm)  (IN_PLACE)               :712"""
+    if len(args) == 3:
+        buf, op, comm = args
+        return Allreduce_(IN_PLACE, buf, _len(buf), op, comm)
+    if len(args) == 4:
+        sendbuf, recvbuf, op, comm = args
+        return Allreduce_(sendbuf, recvbuf, _len(recvbuf), op, comm)
+    sendbuf, recvbuf, count, op, comm = args
+    _assert_minlength(sendbuf, count)
+    _assert_minlength(recvbuf, count)
+    if sendbuf is not IN_PLACE:
+        assert _eltype(sendbuf) == _eltype(recvbuf)
+    T = _eltype(recvbuf)
+    opx = _as_op(op, _torch_dtype(recvbuf))
+    if opx.val is None:
+        return _user_collective("allreduce", sendbuf, recvbuf, count, opx, 0, comm)
+    _stream(comm)
+    _check(lib().mpigx_allreduce(_ptr(sendbuf), _ptr(recvbuf), int(count), T.val, opx.val, comm.val))
+    return recvbuf
+
+
+def Allreduce(sendbuf, op, comm):
+    """collective.jl:733-738: allocating (`similar`) or scalar (`Ref`) form."""
+    torch = _torch()
+    if _is_array(sendbuf):
+        return Allreduce_(sendbuf, torch.empty_like(sendbuf), _len(sendbuf), op, comm)
+    ref = _scalar_ref(sendbuf, comm)
+    out = torch.empty_like(ref)
+    Allreduce_(ref, out, 1, op, comm)
+    return out.item()
+
+
+def _scan_dispatch(args, name):
+    """Scan!/Exscan!(sendbuf, recvbuf, count, op, comm) | (sendbuf, recvbuf, op, comm)
+    | in-place (buf, count, op, comm) | (buf, op, comm).  (collective.jl:760-783 /
+    :834-857 — the reference's in-place forms use an undefined `sendbuf`; here
+    they are the evident IN_PLACE calls.)"""
+    if len(args) == 3:
+        buf, op, comm = args
+        return IN_PLACE, buf, _len(buf), op, comm
+    if len(args) == 4:
+        a, b, c, comm = args
+        if isinstance(b, int) and not _is_array(b):  # (buf, count, op, comm)
+            return IN_PLACE, a, b, c, comm
+        return a, b, _len(a), c, comm
+    return args
+
+
+def _scan_common(args, exclusive):
+    sendbuf, recvbuf, count, op, comm = _scan_dispatch(args, "Exscan!" if exclusive else "Scan!")
+    T = _eltype(recvbuf)
+    opx = _as_op(op, _torch_dtype(recvbuf))
+    if opx.val is None:
+        return _user_collective("exscan" if exclusive else "scan", sendbuf, recvbuf, count, opx, 0, comm)
+    _stream(comm)
+    f = lib().mpigx_exscan if exclusive else lib().mpigx_scan
+    _check(f(_ptr(sendbuf), _ptr(recvbuf), int(count), T.val, opx.val, comm.val))
+    return recvbuf
+
+
+def Scan_(*args):
+    """Inclusive prefix reduction over ranks 0..r — collective.jl:760-783."""
+    return _scan_common(args, False)
+
+
+def Exscan_(*args):
+    """Exclusive prefix reduction; rank 0's recvbuf untouched — collective.jl:834-857."""
+    return _scan_common(args, True)
+
+
+def Scan(sendbuf, op, comm):
+    """collective.jl:803-808."""
+    torch = _torch()
+    if _is_array(sendbuf):
+        return Scan_(sendbuf, torch.empty_like(sendbuf), op, comm)
+    ref = _scalar_ref(sendbuf, comm)
+    out = torch.empty_like(ref)
+    Scan_(ref, out, 1, op, comm)
+    return out.item()
+
+
+def Exscan(sendbuf, op, comm):
+    """collective.jl:877-882 (rank 0's result is undefined: its buffer is untouched)."""
+    torch = _torch()
+    if _is_array(sendbuf):
+        return Exscan_(sendbuf, torch.empty_like(sendbuf), op, comm)
+    ref = _scalar_ref(sendbuf, comm)
+    out = torch.zeros_like(ref)
+    Exscan_(ref, out, 1, op, comm)
+    return out.item()
+
+
+# ---------------------------------------------------------------------------
+# local op (config 2): the built-in MPI.Op set on device buffers
+# ---------------------------------------------------------------------------
+def Reduce_local_(inbuf, inoutbuf, count, op):
+    """MPI_Reduce_local (mpi.h:1357): inoutbuf = op(inoutbuf, inbuf)."""
+    T = _eltype(inoutbuf)
+    opx = _as_op(op, _torch_dtype(inoutbuf))
+    _check(lib().mpigx_reduce_local(_ptr(inbuf), _ptr(inoutbuf), int(count), T.val, opx.val))
+    return inoutbuf
+
+
+def reduce_local_multi(inputs, out, op, order=C.MPIGX_ORDER_MPICH, stream=None, count=None):
+    """out = fold(inputs) as an len(inputs)-rank Allreduce would (asynchronous,
+    on `stream` (torch stream or raw handle; default: current stream))."""
+    torch = _torch()
+    n = len(inputs)
+    arr = (ctypes.c_void_p * n)(*[t.data_ptr() for t in inputs])
+    if stream is None:
+        stream = torch.cuda.current_stream(out.device).cuda_stream
+    elif hasattr(stream, "cuda_stream"):
+        stream = stream.cuda_stream
+    T = _eltype(out)
+    opx = _as_op(op, out.dtype)
+    cnt = out.numel() if count is None else count
+    _check(lib().mpigx_reduce_local_multi(arr, n, ctypes.c_void_p(out.data_ptr()), cnt, T.val, opx.val, order,
+                                          ctypes.c_void_p(stream)))
+    return out

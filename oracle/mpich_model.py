@@ -1,0 +1,410 @@
+"""CPU oracle: a numpy restatement of the arithmetic behind MPI.jl's collectives.
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module, and only as the checker.  The mpigx
+product path never routes through it (there is no CPU fallback).
+
+What it restates
+----------------
+MPI.jl v0.14.2 performs no arithmetic itself: every collective on the hot path
+is one ccall into libmpi (src/collective.jl:34 Bcast, :304 Allgather,
+:498 Alltoall, :615 Reduce, :698 Allreduce, :765 Scan, :839 Exscan).  The
+default libmpi is MPICH 3.3.2 (Project.toml:10 MPICH_jll, deps/build.jl:139-152,
+conf/travis-install-mpi.sh:11 MPICHVER=3.3.2).  MPICH is a third-party
+dependency that is NOT vendored under /root/reference, so this module restates
+its published algorithms (MPICH 3.3.2 src/mpi/coll/...):
+
+* built-in op loops (src/mpi/coll/op/op*.c): ``inout[i] = OP(inout[i], in[i])``
+  with ``MPL_MAX(a,b) = a > b ? a : b``, ``MPL_MIN(a,b) = a < b ? a : b``,
+  ``LAND/LOR/LXOR`` producing 0/1 in the element type, two's-complement wrap
+  for integers, complex PROD as ``(ar*br - ai*bi, ar*bi + ai*br)`` without FMA;
+* MPIR_Allreduce_intra_smp: with MPIR_CVAR_ENABLE_SMP_COLLECTIVES=1 (the
+  MPICH 3.3.2 default, `mpivars`) and every rank on one node, Allreduce is an
+  intra-node MPIR_Reduce to rank 0 followed by MPIR_Bcast, so every rank
+  receives rank 0's reduction (pinned: all ranks' outputs in the fixtures,
+  NaN/±0 cases included);
+* MPIR_Reduce_intra_auto: binomial tree over relative ranks
+  (``relrank = (rank - root) mod n``, the lower subtree is ``inout``) when
+  ``count*size <= 2048`` or ``count < pof2``, else Rabenseifner
+  reduce-scatter (recursive halving) + gather, with the non-power-of-two
+  pre-step in which odd rank ``2i+1`` folds rank ``2i`` into itself
+  (``inout`` = odd);
+* MPIR_Scan / MPIR_Exscan recursive doubling (partial_scan / recvbuf model);
+* Bcast / Allgather / Alltoall are byte copies.
+
+The restatement simulates the message-passing schedule on in-memory per-rank
+buffers, so operand roles (which operand is ``inout``) — which decide NaN and
+signed-zero outcomes of MIN/MAX — are reproduced, not only the association.
+
+Pinning: tests/test_oracle_golden.py checks every function here bit-for-bit
+against tests/golden/mpich_golden.npz, which gen_mpich_golden.c recorded from
+MPICH 3.3.2 itself with the reference's ccall argument shapes.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# ---------------------------------------------------------------------------
+# MPICH handle values (deps/consts_mpich.jl:30-72)
+# ---------------------------------------------------------------------------
+OPS = {
+    "MAX": 1476395009, "MIN": 1476395010, "SUM": 1476395011, "PROD": 1476395012,
+    "LAND": 1476395013, "BAND": 1476395014, "LOR": 1476395015, "BOR": 1476395016,
+    "LXOR": 1476395017, "BXOR": 1476395018,
+}
+OP_NAMES = {v: k for k, v in OPS.items()}
+
+# name -> (handle, numpy dtype, kind); kind in {"int", "uint", "float", "complex", "byte", "bf16", "none"}
+DTYPES = {
+    "INT8_T": (1275068727, np.int8, "int"),
+    "UINT8_T": (1275068731, np.uint8, "uint"),
+    "INT16_T": (1275068984, np.int16, "int"),
+    "UINT16_T": (1275068988, np.uint16, "uint"),
+    "INT32_T": (1275069497, np.int32, "int"),
+    "UINT32_T": (1275069501, np.uint32, "uint"),
+    "INT64_T": (1275070522, np.int64, "int"),
+    "UINT64_T": (1275070526, np.uint64, "uint"),
+    "BYTE": (1275068685, np.uint8, "byte"),
+    "SHORT": (1275068931, np.int16, "int"),
+    "UNSIGNED_SHORT": (1275068932, np.uint16, "uint"),
+    "INT": (1275069445, np.int32, "int"),
+    "UNSIGNED": (1275069446, np.uint32, "uint"),
+    "LONG": (1275070471, np.int64, "int"),
+    "UNSIGNED_LONG": (1275070472, np.uint64, "uint"),
+    "CHAR": (1275068673, np.int8, "int"),
+    "SIGNED_CHAR": (1275068696, np.int8, "int"),
+    "UNSIGNED_CHAR": (1275068674, np.uint8, "uint"),
+    "WCHAR": (1275069454, np.int32, "none"),
+    "FLOAT": (1275069450, np.float32, "float"),
+    "DOUBLE": (1275070475, np.float64, "float"),
+    "C_FLOAT_COMPLEX": (1275070528, np.complex64, "complex"),
+    "C_DOUBLE_COMPLEX": (1275072577, np.complex128, "complex"),
+    # mpigx extension (no MPICH counterpart; parity unpinned): bf16 stored as
+    # uint16 bit patterns, computed in fp32, RNE-rounded after every op.
+    "BFLOAT16": (1275068912, np.uint16, "bf16"),
+}
+DTYPE_BY_HANDLE = {v[0]: k for k, v in DTYPES.items()}
+
+MPI_SUCCESS, MPI_ERR_TYPE, MPI_ERR_OP = 0, 3, 9
+
+ARITH = ("SUM", "PROD")
+ORDERED = ("MIN", "MAX")
+LOGICAL = ("LAND", "LOR", "LXOR")
+BITWISE = ("BAND", "BOR", "BXOR")
+
+
+def op_valid(dtname: str, opname: str) -> int:
+    """Error class MPICH returns for (datatype, op) (op_type_matrix.json pins it).
+
+    SUM/PROD: integers, floats, complex, (CHAR); MIN/MAX/LAND/LOR/LXOR:
+    integers and floats; BAND/BOR/BXOR: integers and BYTE.  WCHAR: nothing.
+    """
+    if dtname not in DTYPES:
+        return MPI_ERR_TYPE
+    if opname not in OPS:
+        return MPI_ERR_OP
+    kind = DTYPES[dtname][2]
+    ok = {
+        "int": True, "uint": True,
+        "float": opname not in BITWISE,
+        "bf16": opname not in BITWISE,
+        "complex": opname in ARITH,
+        "byte": opname in BITWISE,
+        "none": False,
+    }[kind]
+    return MPI_SUCCESS if ok else MPI_ERR_OP
+
+
+# ---------------------------------------------------------------------------
+# bf16 helpers (mpigx definition)
+# ---------------------------------------------------------------------------
+def bf16_to_f32(u16: np.ndarray) -> np.ndarray:
+    return (u16.astype(np.uint32) << 16).view(np.float32)
+
+
+def f32_to_bf16(f: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even fp32 -> bf16; NaN stays NaN (quiet)."""
+    u = np.ascontiguousarray(f, dtype=np.float32).view(np.uint32)
+    nan = (u & 0x7FFFFFFF) > 0x7F800000
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    q = ((u >> 16) | 0x0040).astype(np.uint16)
+    return np.where(nan, q, r)
+
+
+# ---------------------------------------------------------------------------
+# elementwise op: MPIR op loops, a = inout, b = in  ->  new inout
+# ---------------------------------------------------------------------------
+def apply_op(opname: str, dtname: str, inout: np.ndarray, inv: np.ndarray) -> np.ndarray:
+    """``inout[i] = OP(inout[i], in[i])`` exactly as MPICH's MPIR_*_check loops."""
+    kind = DTYPES[dtname][2]
+    if kind == "bf16":
+        a = bf16_to_f32(inout)
+        b = bf16_to_f32(inv)
+        return f32_to_bf16(apply_op(opname, "FLOAT", a, b))
+    a, b = inout, inv
+    with np.errstate(all="ignore"):
+        if opname == "SUM":
+            if kind == "complex":
+                return _cplx(a.real + b.real, a.imag + b.imag, a.dtype)
+            return (a + b).astype(a.dtype)
+        if opname == "PROD":
+            if kind == "complex":
+                # no FMA contraction: each product and sum rounds separately
+                re = a.real * b.real
+                re = re - a.imag * b.imag
+                im = a.real * b.imag
+                im = im + a.imag * b.real
+                return _cplx(re, im, a.dtype)
+            return (a * b).astype(a.dtype)
+        if opname == "MAX":
+            return np.where(a > b, a, b)
+        if opname == "MIN":
+            return np.where(a < b, a, b)
+        if opname == "LAND":
+            return ((a != 0) & (b != 0)).astype(a.dtype)
+        if opname == "LOR":
+            return ((a != 0) | (b != 0)).astype(a.dtype)
+        if opname == "LXOR":
+            return ((a != 0) != (b != 0)).astype(a.dtype)
+        if opname == "BAND":
+            return a & b
+        if opname == "BOR":
+            return a | b
+        if opname == "BXOR":
+            return a ^ b
+    raise ValueError(opname)
+
+
+def _cplx(re, im, dt):
+    out = np.empty(re.shape, dtype=dt)
+    out.real = re
+    out.imag = im
+    return out
+
+
+def reduce_local(inv, inout, dtname, opname):
+    """MPI_Reduce_local(inbuf, inoutbuf, ...) (mpi.h:1357) -> new inoutbuf."""
+    return apply_op(opname, dtname, inout, inv)
+
+
+def _esize(dtname):
+    return np.dtype(DTYPES[dtname][1]).itemsize
+
+
+def _pof2(n):
+    p = 1
+    while p * 2 <= n:
+        p *= 2
+    return p
+
+
+# ---------------------------------------------------------------------------
+# Allreduce: MPIR_Allreduce_intra_smp = Reduce(root 0) + Bcast on one node.
+# (_allreduce_rd is MPIR_Allreduce_intra_recursive_doubling, kept for the
+#  multi-node / SMP-disabled configuration; it is not what one node runs.)
+# ---------------------------------------------------------------------------
+def allreduce(inputs, dtname, opname, short_msg=2048):
+    """Per-rank outputs of MPI_Allreduce (collective.jl:698-700)."""
+    n = len(inputs)
+    res = reduce(inputs, dtname, opname, 0, short_msg)
+    return [res.copy() for _ in range(n)]
+
+
+def _prestep(bufs, dtname, opname, n, pof2):
+    """Non-power-of-two pre-step: odd rank 2i+1 folds rank 2i: inout = odd."""
+    rem = n - pof2
+    for i in range(rem):
+        bufs[2 * i + 1] = apply_op(opname, dtname, bufs[2 * i + 1], bufs[2 * i])
+    newrank = {}
+    for r in range(n):
+        if r < 2 * rem:
+            if r % 2:
+                newrank[r] = r // 2
+        else:
+            newrank[r] = r - rem
+    real = {v: k for k, v in newrank.items()}  # newrank -> rank
+    return rem, newrank, real
+
+
+def _poststep(bufs, n, rem):
+    for i in range(rem):
+        bufs[2 * i] = bufs[2 * i + 1].copy()
+
+
+def _allreduce_rd(inputs, dtname, opname):
+    n = len(inputs)
+    pof2 = _pof2(n)
+    bufs = [x.copy() for x in inputs]
+    rem, newrank, real = _prestep(bufs, dtname, opname, n, pof2)
+    mask = 1
+    while mask < pof2:
+        snap = {nr: bufs[real[nr]].copy() for nr in range(pof2)}
+        for nr in range(pof2):
+            dst = nr ^ mask
+            r = real[nr]
+            # commutative builtin: reduce_local(tmp=partner, recvbuf=own)
+            bufs[r] = apply_op(opname, dtname, snap[nr], snap[dst])
+        mask <<= 1
+    _poststep(bufs, n, rem)
+    return bufs
+
+
+def _allreduce_rsag(inputs, dtname, opname, out_ranks=None):
+    n = len(inputs)
+    count = inputs[0].shape[0]
+    pof2 = _pof2(n)
+    bufs = [x.copy() for x in inputs]
+    rem, newrank, real = _prestep(bufs, dtname, opname, n, pof2)
+    cnts = [count // pof2] * (pof2 - 1) + [count - (count // pof2) * (pof2 - 1)]
+    disps = [0]
+    for i in range(1, pof2):
+        disps.append(disps[-1] + cnts[i - 1])
+    # state per newrank
+    st = {nr: dict(send_idx=0, recv_idx=0, last_idx=pof2) for nr in range(pof2)}
+    mask = 1
+    while mask < pof2:
+        snap = {nr: bufs[real[nr]].copy() for nr in range(pof2)}
+        plan = {}
+        for nr in range(pof2):
+            s = st[nr]
+            dst = nr ^ mask
+            if nr < dst:
+                s["send_idx"] = s["recv_idx"] + pof2 // (mask * 2)
+                lo, hi = s["recv_idx"], s["send_idx"]
+            else:
+                s["recv_idx"] = s["send_idx"] + pof2 // (mask * 2)
+                lo, hi = s["recv_idx"], s["last_idx"]
+            plan[nr] = (dst, disps[lo], (disps[hi] if hi < pof2 else count))
+        for nr in range(pof2):
+            dst, a, b = plan[nr]
+            r = real[nr]
+            seg = apply_op(opname, dtname, snap[nr][a:b], snap[dst][a:b])
+            bufs[r][a:b] = seg
+        for nr in range(pof2):
+            s = st[nr]
+            s["send_idx"] = s["recv_idx"]
+        mask <<= 1
+        if mask < pof2:
+            for nr in range(pof2):
+                s = st[nr]
+                s["last_idx"] = s["recv_idx"] + pof2 // mask
+    # each newrank now owns [disps[recv_idx] .. +block); allgather = copies
+    owned = {}
+    for nr in range(pof2):
+        s = st[nr]
+        lo = s["recv_idx"]
+        a = disps[lo]
+        b = disps[lo + 1] if lo + 1 < pof2 else count
+        owned[nr] = (a, b, bufs[real[nr]][a:b].copy())
+    result = np.empty_like(bufs[0])
+    for nr, (a, b, v) in owned.items():
+        result[a:b] = v
+    return [result.copy() for _ in range(n)]
+
+
+# ---------------------------------------------------------------------------
+# Reduce: MPIR_Reduce_intra_auto (binomial | reduce-scatter + gather)
+# ---------------------------------------------------------------------------
+def reduce(inputs, dtname, opname, root, short_msg=2048):
+    """Result at `root` of MPI_Reduce (collective.jl:615-617)."""
+    n = len(inputs)
+    count = inputs[0].shape[0]
+    pof2 = _pof2(n)
+    if count * _esize(dtname) > short_msg and count >= pof2:
+        return _allreduce_rsag(inputs, dtname, opname)[root]
+    # binomial over relative ranks, lroot = root (commutative builtin)
+    bufs = {rel: inputs[(rel + root) % n].copy() for rel in range(n)}
+    mask = 1
+    while mask < n:
+        for rel in range(n):
+            if rel & (mask - 1):
+                continue  # already sent
+            if (rel & mask) == 0:
+                src = rel | mask
+                if src < n:
+                    bufs[rel] = apply_op(opname, dtname, bufs[rel], bufs[src])
+        mask <<= 1
+    return bufs[0]
+
+
+# ---------------------------------------------------------------------------
+# Scan / Exscan: recursive doubling (MPIR_Scan_intra_recursive_doubling,
+# MPIR_Exscan_intra_recursive_doubling)
+# ---------------------------------------------------------------------------
+def scan(inputs, dtname, opname):
+    n = len(inputs)
+    partial = [x.copy() for x in inputs]
+    recv = [x.copy() for x in inputs]
+    mask = 1
+    while mask < n:
+        snap = [p.copy() for p in partial]
+        for r in range(n):
+            dst = r ^ mask
+            if dst < n:
+                t = snap[dst]
+                if r > dst:
+                    partial[r] = apply_op(opname, dtname, snap[r], t)
+                    recv[r] = apply_op(opname, dtname, recv[r], t)
+                else:
+                    partial[r] = apply_op(opname, dtname, snap[r], t)
+        mask <<= 1
+    return recv
+
+
+def exscan(inputs, dtname, opname, untouched=None):
+    """Per-rank outputs; rank 0's output is `untouched` (its prior recvbuf)."""
+    n = len(inputs)
+    partial = [x.copy() for x in inputs]
+    recv = [None] * n
+    mask = 1
+    while mask < n:
+        snap = [p.copy() for p in partial]
+        for r in range(n):
+            dst = r ^ mask
+            if dst < n:
+                t = snap[dst]
+                partial[r] = apply_op(opname, dtname, snap[r], t)
+                if r > dst and r != 0:
+                    recv[r] = t.copy() if recv[r] is None else apply_op(opname, dtname, recv[r], t)
+        mask <<= 1
+    recv[0] = untouched
+    return recv
+
+
+# ---------------------------------------------------------------------------
+# byte-copy collectives
+# ---------------------------------------------------------------------------
+def bcast(buffers, root):
+    return [buffers[root].copy() for _ in buffers]
+
+
+def allgather(inputs):
+    full = np.concatenate(inputs)
+    return [full.copy() for _ in inputs]
+
+
+def alltoall(inputs, count):
+    n = len(inputs)
+    return [np.concatenate([inputs[j][r * count:(r + 1) * count] for j in range(n)]) for r in range(n)]
+
+
+# ---------------------------------------------------------------------------
+# mpigx-defined folds (no MPICH counterpart), used by the engine's
+# deterministic modes and by the local multi-buffer reduce (config 2)
+# ---------------------------------------------------------------------------
+def fold_linear(inputs, dtname, opname):
+    """Rank-ordered fold ((x0 op x1) op x2) ... with the running value as inout."""
+    v = inputs[0].copy()
+    for x in inputs[1:]:
+        v = apply_op(opname, dtname, v, x)
+    return v
+
+
+def fold_tree(inputs, dtname, opname):
+    """MPICH single-node Allreduce result (binomial tree to rank 0, <= 2 KiB regime)."""
+    return reduce(list(inputs), dtname, opname, 0, short_msg=1 << 62)
+
+
+def fold_rsag(inputs, dtname, opname):
+    """MPICH single-node Allreduce result in the Rabenseifner regime."""
+    return _allreduce_rsag(list(inputs), dtname, opname)[0]

@@ -1,0 +1,216 @@
+"""SPMD parity worker (one process per rank; the reference's test strategy:
+test/runtests.jl runs each test_*.jl under `mpiexec -n nprocs`).
+
+Runs every MPICH golden case recorded at this world size through libmpigx's
+C ABI on device buffers (both algorithms, in-place forms, both reduce
+orders), plus larger seeded cases checked against the oracle, and exits
+non-zero on any mismatch.  Launched by tests/test_collectives_gpu.py.
+"""
+import ctypes
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (ROOT, os.path.join(ROOT, "mpi.jl_amd"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mpigx as MPI  # noqa: E402
+from gen_inputs import make  # noqa: E402
+from golden_io import load, same_bits, typed  # noqa: E402
+from oracle import mpich_model as M  # noqa: E402
+
+IN_PLACE = ctypes.c_void_p(-1 & ((1 << 64) - 1))
+
+
+def dev(a):
+    raw = np.frombuffer(np.ascontiguousarray(a).tobytes(), dtype=np.uint8)
+    t = torch.empty(max(raw.size, 1) + 64, dtype=torch.uint8, device="cuda")[: raw.size]
+    t.copy_(torch.from_numpy(raw.copy()))
+    return t
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def host(t, dt):
+    return t.cpu().numpy().view(dt)
+
+
+class Runner:
+    def __init__(self, comm):
+        self.comm = comm
+        self.L = MPI.lib()
+        self.r = MPI.Comm_rank(comm)
+        self.n = MPI.Comm_size(comm)
+        self.fail = []
+        self.ran = 0
+
+    def check(self, ok, what):
+        self.ran += 1
+        if not ok:
+            self.fail.append(what)
+
+    def run(self, coll, ins, dtname, opname, count, root=0, inplace=False):
+        """Run one collective on my input ins[r]; return my output (numpy) or None."""
+        L, r, n, cv = self.L, self.r, self.n, self.comm.val
+        npdt = M.DTYPES[dtname][1]
+        h = M.DTYPES[dtname][0]
+        op = M.OPS.get(opname, 0) if opname else 0
+        x = ins[r]
+        if coll in ("allreduce", "scan", "exscan"):
+            recv = dev(x) if inplace else dev(np.full(x.size * x.itemsize, 0xCD, np.uint8))
+            send = IN_PLACE if inplace else P(dev(x))
+            f = {"allreduce": L.mpigx_allreduce, "scan": L.mpigx_scan, "exscan": L.mpigx_exscan}[coll]
+            rc = f(send, P(recv), count, h, op, cv)
+            assert rc == 0, (coll, rc)
+            return host(recv, npdt)
+        if coll == "reduce":
+            isroot = r == root
+            if inplace and isroot:
+                recv = dev(x)
+                rc = L.mpigx_reduce(IN_PLACE, P(recv), count, h, op, root, cv)
+            else:
+                recv = dev(np.zeros_like(x)) if isroot else None
+                rc = L.mpigx_reduce(P(dev(x)), P(recv), count, h, op, root, cv)
+            assert rc == 0, (coll, rc)
+            return host(recv, npdt) if isroot else None
+        if coll == "bcast":
+            buf = dev(x)
+            rc = L.mpigx_bcast(P(buf), count, h, root, cv)
+            assert rc == 0
+            return host(buf, npdt)
+        if coll == "allgather":
+            if inplace:
+                full = np.zeros(count * n, dtype=npdt)
+                full[r * count:(r + 1) * count] = x
+                recv = dev(full)
+                rc = L.mpigx_allgather(IN_PLACE, 0, 0, P(recv), count, h, cv)
+            else:
+                recv = dev(np.zeros(count * n, dtype=npdt))
+                rc = L.mpigx_allgather(P(dev(x)), count, h, P(recv), count, h, cv)
+            assert rc == 0
+            return host(recv, npdt)
+        if coll == "alltoall":
+            if inplace:
+                recv = dev(x)
+                rc = L.mpigx_alltoall(IN_PLACE, 0, 0, P(recv), count, h, cv)
+            else:
+                recv = dev(np.zeros(count * n, dtype=npdt))
+                rc = L.mpigx_alltoall(P(dev(x)), count, h, P(recv), count, h, cv)
+            assert rc == 0
+            return host(recv, npdt)
+        raise KeyError(coll)
+
+    def golden(self):
+        cases, arr = load()
+        for c in cases:
+            if c["n"] != self.n or c["coll"] == "reduce_local":
+                continue
+            npdt = M.DTYPES[c["dtype"]][1]
+            ins = typed(arr[c["id"] + ".in"], npdt)
+            outs = typed(arr[c["id"] + ".out"], npdt)
+            coll = c["coll"]
+            algos = ("oneshot", "twoshot") if coll in ("allreduce", "reduce") else ("auto",)
+            for algo in algos:
+                os.environ["MPIGX_ALGO"] = algo
+                for inplace in (False, True):
+                    if inplace and coll in ("bcast",):
+                        continue
+                    got = self.run(coll, ins, c["dtype"], c["op"], c["count"], c["root"], inplace)
+                    exp = outs[self.r]
+                    if coll == "reduce" and self.r != c["root"]:
+                        continue
+                    if coll == "exscan" and self.r == 0:
+                        if not inplace:  # untouched 0xCD sentinel, like MPICH
+                            self.check(np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (c["id"], algo, "rank0"))
+                        continue
+                    self.check(same_bits(got, exp), (c["id"], coll, c["dtype"], c["op"], algo, inplace))
+        os.environ.pop("MPIGX_ALGO", None)
+
+    def oracle_cases(self, sizes):
+        """Larger seeded cases vs the (MPICH-pinned) oracle."""
+        n, r = self.n, self.r
+        for i, (dtname, opname, count) in enumerate(sizes):
+            ins = make(dtname, opname, n, count, 1000 + i, edge=opname in ("MAX", "MIN"))
+            for algo in ("oneshot", "twoshot"):
+                os.environ["MPIGX_ALGO"] = algo
+                got = self.run("allreduce", ins, dtname, opname, count)
+                self.check(same_bits(got, M.allreduce(ins, dtname, opname)[r]), ("oracle-allreduce", dtname, opname, count, algo))
+                root = (i + 1) % n
+                got = self.run("reduce", ins, dtname, opname, count, root=root)
+                if r == root:
+                    self.check(same_bits(got, M.reduce(ins, dtname, opname, root)), ("oracle-reduce", dtname, opname, count, algo))
+            os.environ.pop("MPIGX_ALGO", None)
+            got = self.run("scan", ins, dtname, opname, count)
+            self.check(same_bits(got, M.scan(ins, dtname, opname)[r]), ("oracle-scan", dtname, opname, count))
+            got = self.run("exscan", ins, dtname, opname, count)
+            if r > 0:
+                self.check(same_bits(got, M.exscan(ins, dtname, opname)[r]), ("oracle-exscan", dtname, opname, count))
+        # byte movers at sizes that span several blocks
+        for count in (1, 4097, 300001):
+            ins = make("FLOAT", "SUM", n, count * n, 77 + count)
+            got = self.run("alltoall", ins, "FLOAT", None, count)
+            self.check(same_bits(got, M.alltoall(ins, count)[r]), ("alltoall", count))
+            ins1 = [x[:count] for x in ins]
+            got = self.run("allgather", ins1, "FLOAT", None, count)
+            self.check(same_bits(got, M.allgather(ins1)[r]), ("allgather", count))
+            got = self.run("bcast", ins1, "FLOAT", None, count, root=n - 1)
+            self.check(same_bits(got, ins1[n - 1]), ("bcast", count))
+
+    def linear_order(self):
+        MPI.set_reduce_order(self.comm, 1)
+        for i, (dtname, opname, count) in enumerate((("FLOAT", "SUM", 5000), ("DOUBLE", "SUM", 70001),
+                                                    ("FLOAT", "MAX", 3000), ("BFLOAT16", "SUM", 9999))):
+            ins = make(dtname, opname, self.n, count, 500 + i, edge=opname == "MAX")
+            for algo in ("oneshot", "twoshot"):
+                os.environ["MPIGX_ALGO"] = algo
+                got = self.run("allreduce", ins, dtname, opname, count)
+                self.check(same_bits(got, M.fold_linear(ins, dtname, opname)), ("linear", dtname, opname, algo))
+        os.environ.pop("MPIGX_ALGO", None)
+        MPI.set_reduce_order(self.comm, 0)
+
+    def errors(self):
+        L, cv = self.L, self.comm.val
+        t = dev(np.zeros(16, np.float32))
+        self.check(L.mpigx_allreduce(P(t), P(t), 4, M.DTYPES["FLOAT"][0], M.OPS["BAND"], cv) == 9, "err-op")
+        self.check(L.mpigx_allreduce(P(t), P(t), 4, 42, M.OPS["SUM"], cv) == 3, "err-type")
+        self.check(L.mpigx_allreduce(P(t), P(t), -1, M.DTYPES["FLOAT"][0], M.OPS["SUM"], cv) == 2, "err-count")
+        self.check(L.mpigx_reduce(P(t), P(t), 4, M.DTYPES["FLOAT"][0], M.OPS["SUM"], self.n, cv) == 7, "err-root")
+        self.check(L.mpigx_bcast(P(t), 4, M.DTYPES["FLOAT"][0], -1, cv) == 7, "err-root-bcast")
+        self.check(L.mpigx_allreduce(None, None, 0, M.DTYPES["FLOAT"][0], M.OPS["SUM"], cv) == 0, "count0")
+
+
+def main():
+    comm = MPI.Init()
+    R = Runner(comm)
+    phase = os.environ.get("MPIGX_TEST_PHASE", "all")
+    R.golden()
+    R.errors()
+    R.oracle_cases([("FLOAT", "SUM", 1_000_003), ("DOUBLE", "SUM", 65537), ("FLOAT", "MAX", 100_001),
+                    ("INT32_T", "BAND", 262_147), ("INT64_T", "MAX", 50_000), ("BFLOAT16", "SUM", 40_000),
+                    ("C_FLOAT_COMPLEX", "PROD", 3333), ("UINT8_T", "BXOR", 100_000)])
+    R.linear_order()
+    if phase == "all":
+        # rounds: a communicator whose staging arena is 1 MiB forces multi-round launches
+        os.environ["MPIGX_STAGING_BYTES"] = str(1 << 20)
+        c2 = MPI.Comm_dup(comm)
+        R2 = Runner(c2)
+        R2.oracle_cases([("FLOAT", "SUM", 700_001), ("DOUBLE", "MIN", 300_001)])
+        MPI.free(c2)
+        R.fail += R2.fail
+        R.ran += R2.ran
+    MPI.Barrier(comm)
+    MPI.Finalize()
+    print(json.dumps({"rank": R.r, "n": R.n, "checks": R.ran, "failures": [str(f) for f in R.fail[:20]],
+                      "nfail": len(R.fail)}), flush=True)
+    sys.exit(1 if R.fail else 0)
+
+
+if __name__ == "__main__":
+    main()

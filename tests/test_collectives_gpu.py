@@ -1,0 +1,25 @@
+"""Multi-rank parity on device buffers: every MPICH golden case at n ranks,
+plus oracle-checked larger cases, in-place forms, LINEAR order, multi-round
+staging and error classes (tests/spmd/golden_worker.py).
+
+On the 1-GPU test box all ranks share cuda:0 and talk through hipIpc
+exactly as they do across GPUs (peer-mapped HBM, uncached signal arrays);
+grids are capped (MPIGX_MAX_BLOCKS) so every rank's blocks are co-resident.
+"""
+import os
+
+import pytest
+
+from spmd_launch import ROOT, launch
+
+pytestmark = pytest.mark.gpu
+
+ENV = {"MPIGX_DEVICE": "0", "MPIGX_MAX_BLOCKS": "16", "MPIGX_TIMEOUT_MS": "30000",
+       "MPIGX_STAGING_BYTES": str(64 << 20)}
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 8])
+def test_golden_collectives(n):
+    rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "golden_worker.py"), n, timeout=900, extra_env=ENV)
+    msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
+    assert all(rc == 0 for rc in rcs), msg

@@ -1,0 +1,137 @@
+"""Config 2 parity: the device MPI.Op kernels (mpigx_reduce_local_multi /
+mpigx_reduce_local) against the MPICH-pinned oracle, bit for bit.
+
+The fold of n buffers must equal what an n-rank MPICH Allreduce returns
+(binomial regime <= 2 KiB, Rabenseifner regime above, operand roles
+included), or the rank-ordered left fold in LINEAR order.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from gen_inputs import make, valid_pairs
+from golden_io import same_bits
+from oracle import mpich_model as M
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+REPRESENTATIVE = ["INT8_T", "UINT8_T", "INT16_T", "UINT16_T", "INT32_T", "UINT32_T", "INT64_T", "UINT64_T",
+                  "BYTE", "CHAR", "LONG", "FLOAT", "DOUBLE", "C_FLOAT_COMPLEX", "C_DOUBLE_COMPLEX", "BFLOAT16"]
+
+
+@pytest.fixture(scope="module")
+def L():
+    import mpigx
+    assert torch.cuda.is_available()
+    return mpigx.lib()
+
+
+def dev(a, pad=0):
+    """numpy -> device uint8 tensor (optionally starting `pad` bytes into an allocation)."""
+    raw = np.frombuffer(a.tobytes(), dtype=np.uint8)
+    t = torch.empty(raw.size + pad + 16, dtype=torch.uint8, device="cuda")
+    v = t[pad:pad + raw.size]
+    v.copy_(torch.from_numpy(raw.copy()))
+    return v
+
+
+def host(t, like, count):
+    return t.cpu().numpy().view(like.dtype)[:count]
+
+
+def run_multi(L, ins, dtname, opname, order, pad=0):
+    count = ins[0].size
+    h = M.DTYPES[dtname][0]
+    dins = [dev(x, pad) for x in ins]
+    out = dev(np.zeros_like(ins[0]), pad)
+    ptrs = (ctypes.c_void_p * len(ins))(*[t.data_ptr() for t in dins])
+    rc = L.mpigx_reduce_local_multi(ptrs, len(ins), ctypes.c_void_p(out.data_ptr()), count, h, M.OPS[opname],
+                                    order, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    return host(out, ins[0], count)
+
+
+def expected(ins, dtname, opname, order):
+    if order == 1:
+        return M.fold_linear(ins, dtname, opname)
+    return M.allreduce(ins, dtname, opname)[0]
+
+
+@pytest.mark.parametrize("dtname,opname", valid_pairs(REPRESENTATIVE))
+def test_all_ops_types(L, dtname, opname):
+    for n, count, seed in ((8, 1037, 1), (3, 517, 2), (5, 4099, 3), (2, 64, 4)):
+        ins = make(dtname, opname, n, count, seed, edge=True)
+        for order in (0, 1):
+            got = run_multi(L, ins, dtname, opname, order)
+            assert same_bits(got, expected(ins, dtname, opname, order)), (n, count, order)
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 6, 7, 9, 12, 16])
+def test_rank_counts(L, n):
+    for dtname, opname in (("FLOAT", "SUM"), ("FLOAT", "MAX"), ("INT64_T", "BXOR"), ("DOUBLE", "MIN")):
+        for count in (7, 300, 20011):
+            ins = make(dtname, opname, n, count, 10 + n, edge=True)
+            for order in (0, 1):
+                got = run_multi(L, ins, dtname, opname, order)
+                assert same_bits(got, expected(ins, dtname, opname, order)), (dtname, opname, n, count, order)
+
+
+def test_unaligned_and_empty(L):
+    ins = make("FLOAT", "SUM", 8, 1001, 7)
+    for pad in (1, 4, 8, 12):
+        got = run_multi(L, ins, "FLOAT", "SUM", 0, pad=pad)
+        assert same_bits(got, expected(ins, "FLOAT", "SUM", 0)), pad
+    empty = [np.zeros(0, np.float32)] * 4
+    ptrs = (ctypes.c_void_p * 4)(*([0] * 4))
+    assert L.mpigx_reduce_local_multi(ptrs, 4, None, 0, M.DTYPES["FLOAT"][0], M.OPS["SUM"], 0, None) == 0
+
+
+def test_invalid_pairs_rejected(L):
+    t = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    ptrs = (ctypes.c_void_p * 2)(t.data_ptr(), t.data_ptr())
+    for dtname, opname, code in (("FLOAT", "BAND", 9), ("C_FLOAT_COMPLEX", "MAX", 9), ("BYTE", "SUM", 9),
+                                 ("WCHAR", "SUM", 9)):
+        rc = L.mpigx_reduce_local_multi(ptrs, 2, ctypes.c_void_p(t.data_ptr()), 4, M.DTYPES[dtname][0],
+                                        M.OPS[opname], 0, None)
+        assert rc == code
+    assert L.mpigx_reduce_local_multi(ptrs, 2, ctypes.c_void_p(t.data_ptr()), 4, 12345, M.OPS["SUM"], 0,
+                                      None) == 3
+
+
+def test_reduce_local_matches_mpich_fixtures(L):
+    """MPI_Reduce_local golden vectors (MPICH 3.3.2) through mpigx_reduce_local."""
+    from golden_io import load, typed
+    cases, arr = load()
+    bad = []
+    for c in cases:
+        if c["coll"] != "reduce_local":
+            continue
+        dt = M.DTYPES[c["dtype"]][1]
+        a, b = typed(arr[c["id"] + ".in"], dt)
+        exp = typed(arr[c["id"] + ".out"], dt)[0]
+        din, dio = dev(a), dev(b)
+        rc = L.mpigx_reduce_local(ctypes.c_void_p(din.data_ptr()), ctypes.c_void_p(dio.data_ptr()), c["count"],
+                                  M.DTYPES[c["dtype"]][0], M.OPS[c["op"]])
+        assert rc == 0
+        if not same_bits(host(dio, b, c["count"]), exp):
+            bad.append(c["id"])
+    assert not bad, bad
+
+
+@pytest.mark.slow
+def test_full_size_property(L):
+    """Config 2 at full size (8 x 256 MiB f32): SUM of (k+1)*ones in bf16-exact
+    integers is exact, and linearity across two calls holds."""
+    n, count = 8, 64 << 20
+    ins = [torch.full((count,), float(k + 1), device="cuda") for k in range(n)]
+    out = torch.empty(count, device="cuda")
+    import mpigx
+    mpigx.reduce_local_multi(ins, out, mpigx.SUM)
+    torch.cuda.synchronize()
+    assert torch.all(out == 36.0)
+    mpigx.reduce_local_multi(ins, out, mpigx.MAX)
+    torch.cuda.synchronize()
+    assert torch.all(out == 8.0)
