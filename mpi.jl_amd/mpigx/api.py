@@ -298,9 +298,9 @@ def _bootstrap_id(rank, size):
     if not dist.is_initialized():
         dist.init_process_group("gloo", rank=rank, world_size=size)
         _state["pg_owned"] = True
-    obj = [bytes(uid.internal) if rank == 0 else None]
+    obj = [ctypes.string_at(ctypes.addressof(uid), 128) if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
-    ctypes.memmove(uid.internal, obj[0], 128)
+    ctypes.memmove(ctypes.addressof(uid), bytes(obj[0]), 128)
     return uid
 
 
@@ -381,9 +381,9 @@ def Comm_dup(comm: Comm) -> Comm:
     uid = UniqueId()
     if comm._rank == 0:
         _check(lib().mpigx_get_unique_id(ctypes.byref(uid)))
-    t = torch.frombuffer(bytearray(uid.internal), dtype=torch.uint8).to(f"cuda:{comm.device}")
+    t = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(uid), 128)), dtype=torch.uint8).to(f"cuda:{comm.device}")
     Bcast_(t, 0, comm)
-    ctypes.memmove(uid.internal, bytes(t.cpu().numpy().tobytes()), 128)
+    ctypes.memmove(ctypes.addressof(uid), bytes(t.cpu().numpy().tobytes()), 128)
     h = ctypes.c_void_p()
     _check(lib().mpigx_comm_init_rank(ctypes.byref(h), comm._size, ctypes.byref(uid), comm._rank, comm.device))
     return Comm(h, comm._rank, comm._size, comm.device)

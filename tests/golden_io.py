@@ -24,10 +24,15 @@ def typed(raw_rows, npdtype):
     return [np.ascontiguousarray(r).view(npdtype) for r in raw_rows]
 
 
-def same_bits(a, b):
-    """Bitwise equality, except any NaN matches any NaN (payloads differ by ISA)."""
+def same_bits(a, b, bf16=False):
+    """Bitwise equality, except any NaN matches any NaN (payloads and the sign
+    of a generated NaN differ by ISA: x86 default NaN is 0xFFC00000, AMDGPU
+    0x7FC00000).  bf16=True compares uint16 bf16 patterns that way too."""
     a = np.asarray(a)
     b = np.asarray(b)
+    if bf16:
+        a = (a.astype(np.uint32) << 16).view(np.float32)
+        b = (b.astype(np.uint32) << 16).view(np.float32)
     if a.shape != b.shape:
         return False
     if a.dtype.kind in "fc":

@@ -14,7 +14,7 @@ from spmd_launch import ROOT, launch
 
 pytestmark = pytest.mark.gpu
 
-ENV = {"MPIGX_DEVICE": "0", "MPIGX_MAX_BLOCKS": "16", "MPIGX_TIMEOUT_MS": "30000",
+ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_MAX_BLOCKS": "16", "MPIGX_TIMEOUT_MS": "30000",
        "MPIGX_STAGING_BYTES": str(64 << 20)}
 
 
@@ -23,3 +23,16 @@ def test_golden_collectives(n):
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "golden_worker.py"), n, timeout=900, extra_env=ENV)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     assert all(rc == 0 for rc in rcs), msg
+    summ = _summaries(outs)
+    assert len(summ) == n and all(x["nfail"] == 0 and x["checks"] > 200 for x in summ), summ
+    print(summ[0])
+
+
+def _summaries(outs):
+    import json
+    res = []
+    for o in outs:
+        for line in o.splitlines():
+            if line.startswith("{") and '"checks"' in line:
+                res.append(json.loads(line))
+    return res

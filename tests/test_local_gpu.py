@@ -66,7 +66,7 @@ def test_all_ops_types(L, dtname, opname):
         ins = make(dtname, opname, n, count, seed, edge=True)
         for order in (0, 1):
             got = run_multi(L, ins, dtname, opname, order)
-            assert same_bits(got, expected(ins, dtname, opname, order)), (n, count, order)
+            assert same_bits(got, expected(ins, dtname, opname, order), dtname == "BFLOAT16"), (n, count, order)
 
 
 @pytest.mark.parametrize("n", [1, 2, 4, 6, 7, 9, 12, 16])
@@ -76,7 +76,7 @@ def test_rank_counts(L, n):
             ins = make(dtname, opname, n, count, 10 + n, edge=True)
             for order in (0, 1):
                 got = run_multi(L, ins, dtname, opname, order)
-                assert same_bits(got, expected(ins, dtname, opname, order)), (dtname, opname, n, count, order)
+                assert same_bits(got, expected(ins, dtname, opname, order), dtname == "BFLOAT16"), (dtname, opname, n, count, order)
 
 
 def test_unaligned_and_empty(L):
