@@ -175,7 +175,10 @@ template <class OP, class T> struct role_sensitive {
 // 16-byte register vector for the streaming paths
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef MPIGX_NT
-#define MPIGX_NT 1  // non-temporal hints on streamed (read-once) data
+#define MPIGX_NT 1  // non-temporal hints on streamed (read-once) loads
+#endif
+#ifndef MPIGX_NT_STORE
+#define MPIGX_NT_STORE 0  // fold outputs: plain stores measured >= nt (tools/local_tune.hip)
 #endif
 __device__ __forceinline__ u32x4 ld16(const void* p) {
 #if MPIGX_NT
@@ -185,7 +188,7 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
 #endif
 }
 __device__ __forceinline__ void st16(void* p, u32x4 v) {
-#if MPIGX_NT
+#if MPIGX_NT_STORE
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
 #else
   *reinterpret_cast<u32x4*>(p) = v;
