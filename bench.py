@@ -183,6 +183,8 @@ def bench_local(args):
 
 
 def bench_allreduce(args):
+    import ctypes
+
     import torch
     import torch.distributed as dist
     import mpigx as MPI
@@ -194,43 +196,92 @@ def bench_allreduce(args):
     dist.init_process_group("gloo", rank=rank, world_size=n)
     comm = MPI.Init()
     dev = torch.device(f"cuda:{local}")
-    count = args.mib << 18
-    S = count * 4
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    send = torch.rand(count, device=dev, generator=g) * 2 - 1
-    recv = torch.empty_like(send)
     stream = torch.cuda.current_stream(dev)
 
-    for _ in range(args.warmup):
-        MPI.Allreduce_(send, recv, MPI.SUM, comm)
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
-        MPI.Allreduce_(send, recv, MPI.SUM, comm)
-        b.record(stream)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t = (time.perf_counter() - t0) / args.steps
-    kern = sum(a.elapsed_time(b) for a, b in ev) / args.steps / 1e3
-    tt = torch.tensor([t, kern], dtype=torch.float64)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t, kern = tt.tolist()
-    # correctness: SUM over ranks of a rank-seeded pattern (exact in f32)
-    chk = torch.full((4096,), float(rank + 1), device=dev)
+    def tmax(*xs):
+        tt = torch.tensor(list(xs), dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return tt.tolist()
+
+    def time_ar(nbytes, steps, warmup, fn=None):
+        """(wall s/step, device s/step) of blocking Allreduce!(SUM) f32, max over ranks."""
+        count = nbytes // 4
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        send = torch.rand(count, device=dev, generator=g) * 2 - 1
+        recv = torch.empty_like(send)
+        call = fn or (lambda: MPI.Allreduce_(send, recv, MPI.SUM, comm))
+        if fn is not None:
+            call = lambda: fn(send, recv)  # noqa: E731
+        for _ in range(warmup):
+            call()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for a, b in ev:
+            a.record(stream)
+            call()
+            b.record(stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        wall = (time.perf_counter() - t0) / steps
+        kern = sum(a.elapsed_time(b) for a, b in ev) / steps / 1e3
+        return tmax(wall, kern)
+
+    def busbw(nbytes, t):
+        return nbytes / t * 2 * (n - 1) / n / 1e9
+
+    S = args.mib << 20
+    t, kern = time_ar(S, args.steps, args.warmup)
+
+    # correctness on the timed path: SUM of rank-constant data is exact in f32
+    chk = torch.full((1 << 20,), float(rank + 1), device=dev)
     out = torch.empty_like(chk)
     MPI.Allreduce_(chk, out, MPI.SUM, comm)
     ok = bool(torch.all(out == n * (n + 1) / 2).item())
-    busbw = S / t * 2 * (n - 1) / n / 1e9
-    peak = XGMI_LINK_GBPS * (n - 1)
-    ach = S / kern * 2 * (n - 1) / n / 1e9
+
+    # measured xGMI: every rank pulls 64 MiB from every peer at once / from one peer
+    probe = {}
+    for kind, name in ((0, "all_peers"), (1, "one_link")):
+        secs = ctypes.c_double(0)
+        pb = 64 << 20
+        MPI.lib().mpigx_comm_probe(comm.val, kind, pb, ctypes.byref(secs))  # warm
+        MPI.lib().mpigx_comm_probe(comm.val, kind, pb, ctypes.byref(secs))
+        (sec,) = tmax(secs.value)
+        probe[name + "_GBps"] = round(pb * ((n - 1) if kind == 0 else 1) / sec / 1e9, 1)
+
+    # size sweep (mpigx) and the RCCL comparison point (torch.distributed nccl = RCCL)
+    sweep, rccl = {}, {}
+    sizes = [1 << 20, 16 << 20, 64 << 20, S, 1 << 30]
+    for nb in sizes:
+        tw, tk = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
+        sweep[f"{nb >> 20}MiB"] = {"busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1),
+                                   "ms": round(tw * 1e3, 4)}
+    for nb in (1 << 20, 16 << 20):
+        for algo in ("oneshot", "twoshot"):
+            os.environ["MPIGX_ALGO"] = algo
+            tw, _ = time_ar(nb, 10, 2)
+            sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
+        os.environ.pop("MPIGX_ALGO", None)
+    try:
+        ng = dist.new_group(backend="nccl")
+        for nb in sizes:
+            tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2,
+                            fn=lambda s_, r_: (r_.copy_(s_), dist.all_reduce(r_, group=ng)))
+            rccl[f"{nb >> 20}MiB"] = round(busbw(nb, tw), 1)
+    except Exception as e:  # noqa: BLE001
+        rccl = {"error": str(e)[:200]}
+
+    value = busbw(S, t)
+    ach = busbw(S, kern)
+    peak_meas = probe.get("all_peers_GBps")
+    peak_nom = XGMI_LINK_GBPS * (n - 1)
+    peak = peak_meas if peak_meas else peak_nom
     if rank == 0:
         res = {
             "metric": "Allreduce! busbw GB/s (256MiB f32 SUM) at 1/2/4/8 GPUs; % of xGMI/HBM peak",
-            "value": round(busbw, 2), "unit": "GB/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (uniform[-1,1) f32 per rank, seeded, resident in HBM)",
             "config": {"workload": f"config 3 at {args.mib} MiB: MPI.Allreduce!(SUM) f32, blocking, {n} ranks",
@@ -238,9 +289,14 @@ def bench_allreduce(args):
                        "bytes_per_rank": S, "algbw_GBps": round(S / t / 1e9, 2)},
             "roofline": {"bound": "xgmi", "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
                          "frac": round(ach / peak, 4), "traffic": None,
-                         "peak_basis": f"{n - 1} links x {XGMI_LINK_GBPS} GB/s per direction (nominal)"},
+                         "peak_basis": "measured: every rank pulling from all peers at once (mpigx_comm_probe)"
+                                       if peak_meas else f"nominal {n - 1} x {XGMI_LINK_GBPS} GB/s",
+                         "peak_nominal": peak_nom},
             "cpu_baseline": None,
             "correct": ok,
+            "xgmi_probe": probe,
+            "sweep_mpigx_busbw": sweep,
+            "rccl_busbw": rccl,
         }
         print(json.dumps(res), flush=True)
     MPI.Finalize()

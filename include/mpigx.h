@@ -132,6 +132,12 @@ int mpigx_comm_set_blocking(mpigx_comm_t comm, int blocking);
 int mpigx_comm_synchronize(mpigx_comm_t comm);
 int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
 
+/* Diagnostic (bench roofline denominator): every rank pulls `bytes` from
+ * every peer's staging arena at once (kind 0: aggregate xGMI ingress) or
+ * from rank+1 only (kind 1: one link).  *seconds = device time of the pull
+ * (includes one cross-rank barrier).  Collective. */
+int mpigx_comm_probe(mpigx_comm_t comm, int kind, long long bytes, double *seconds);
+
 /* ---- collectives (src/collective.jl ccall sites) ------------------------- */
 /* MPI_Barrier  — collective.jl:15-19 */
 int mpigx_barrier(mpigx_comm_t comm);

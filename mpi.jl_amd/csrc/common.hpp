@@ -40,7 +40,7 @@ enum FoldMode : int {
 };
 
 // Copy-kernel modes (Bcast / Allgather / Alltoall / Barrier).
-enum CopyMode : int { C_BCAST = 0, C_ALLGATHER = 1, C_ALLTOALL = 2, C_BARRIER = 3 };
+enum CopyMode : int { C_BCAST = 0, C_ALLGATHER = 1, C_ALLTOALL = 2, C_BARRIER = 3, C_PROBE_ALL = 4, C_PROBE_ONE = 5 };
 
 // Per-call view of the communicator, passed by value to every kernel.
 struct PeerView {

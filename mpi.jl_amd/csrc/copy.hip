@@ -14,6 +14,26 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
     rank_barrier(pv, ep);
     return;
   }
+  if (A.mode == C_PROBE_ALL || A.mode == C_PROBE_ONE) {
+    // xGMI probe: pull A.bytes from every peer's staging (PROBE_ALL: all
+    // links at once = aggregate ingress) or from rank r+1 only (one link);
+    // loads are folded into a register so they stay live.
+    if (!rank_barrier(pv, ep++)) return;
+    const long long lo = lmin((long long)b * A.slice, A.bytes), hi = lmin(lo + A.slice, A.bytes);
+    u32x4 acc = {0, 0, 0, 0};
+    for (int k = 1; k < n; ++k) {
+      if (A.mode == C_PROBE_ONE && k > 1) break;
+      const u32x4* s = reinterpret_cast<const u32x4*>(pv.stage[(r + k) % n] + lo);
+      const long long nv = (hi - lo) / 16;
+      long long i = threadIdx.x;
+      for (; i + 3 * (long long)blockDim.x < nv; i += 4 * (long long)blockDim.x)
+        acc ^= ld16(s + i) ^ ld16(s + i + blockDim.x) ^ ld16(s + i + 2 * blockDim.x) ^ ld16(s + i + 3 * blockDim.x);
+      for (; i < nv; i += blockDim.x) acc ^= ld16(s + i);
+    }
+    if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u) reinterpret_cast<u32x4*>(pv.stage[r])[threadIdx.x] = acc;
+    rank_barrier(pv, ep++);
+    return;
+  }
   const long long lo = lmin((long long)b * A.slice, A.bytes), hi = lmin(lo + A.slice, A.bytes);
   const long long len = hi - lo;
   char* mine = pv.stage[r];

@@ -631,6 +631,35 @@ int mpigx_barrier(mpigx_comm_t c) {
   return finish(c);
 }
 
+int mpigx_comm_probe(mpigx_comm_t c, int kind, long long bytes, double* seconds) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  if (c->n == 1 || bytes <= 0) return MPIGX_ERR_ARG;
+  if ((size_t)bytes > c->stage_bytes) bytes = (long long)c->stage_bytes;
+  bytes &= ~15ll;
+  CopyArgs a;
+  memset(&a, 0, sizeof a);
+  a.pv = make_view(c);
+  a.mode = kind == 1 ? C_PROBE_ONE : C_PROBE_ALL;
+  a.bytes = bytes;
+  const int g = c->max_blocks;
+  a.slice = rup(cdiv(bytes, g), 16);
+  hipEvent_t e0, e1;
+  HIPCK(hipEventCreate(&e0));
+  HIPCK(hipEventCreate(&e1));
+  HIPCK(hipEventRecord(e0, c->stream));
+  HIPCK(launch_copy(dim3(g), c->stream, a));
+  HIPCK(hipEventRecord(e1, c->stream));
+  c->epoch += 2;
+  HIPCK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (seconds) *seconds = ms / 1e3;
+  return finish(c);
+}
+
 int mpigx_bcast(void* buf, int count, int datatype, int root, mpigx_comm_t c) {
   int rc = check_comm(c);
   if (rc) return rc;

@@ -1,0 +1,122 @@
+"""CPU-only checks of the drop-in boundary (no GPU calls):
+
+* libmpigx.so loads and exports every function include/mpigx.h declares;
+* handle/error constants in the header are MPICH's (deps/consts_mpich.jl,
+  mpi.h:782-809) and agree with the Python mirror and the oracle;
+* host-side validation (mpigx_op_valid / mpigx_type_size) reproduces MPICH's
+  op x type matrix recorded in tests/golden/op_type_matrix.json.
+"""
+import ctypes
+import re
+
+import pytest
+
+import mpigx
+from golden_io import op_type_matrix
+from mpigx import consts as C
+from oracle import mpich_model as M
+
+
+def header_text():
+    with open(mpigx.HEADER_PATH) as f:
+        return f.read()
+
+
+def declared_functions():
+    txt = re.sub(r"/\*.*?\*/", "", header_text(), flags=re.S)
+    return sorted(set(re.findall(r"^\s*int\s+(mpigx_\w+)\s*\(", txt, flags=re.M)))
+
+
+def header_defines():
+    return {k: int(v) for k, v in re.findall(r"#define\s+(MPIGX_\w+)\s+(-?\d+)\s*$", header_text(), flags=re.M)}
+
+
+def test_library_exports_every_declared_symbol():
+    L = mpigx.lib()
+    fns = declared_functions()
+    assert len(fns) >= 25
+    missing = [f for f in fns if not hasattr(L, f)]
+    assert not missing, missing
+    # and the Python binding declares prototypes for all of them
+    from mpigx._lib import PROTOTYPES
+    assert sorted(PROTOTYPES) == fns
+
+
+def test_constants_match_mpich():
+    d = header_defines()
+    for name, (handle, _, kind) in M.DTYPES.items():
+        assert d[f"MPIGX_{name}"] == handle, name
+        assert getattr(C, f"MPI_{name}" if name != "BFLOAT16" else "MPIGX_BFLOAT16") == handle
+    for name, handle in M.OPS.items():
+        assert d[f"MPIGX_{name}"] == handle == getattr(C, f"MPI_{name}")
+    for cls in ("SUCCESS", "ERR_BUFFER", "ERR_COUNT", "ERR_TYPE", "ERR_COMM", "ERR_ROOT", "ERR_OP", "ERR_ARG",
+                "ERR_OTHER", "ERR_INTERN"):
+        assert d[f"MPIGX_{cls}"] == getattr(C, f"MPI_{cls}")
+
+
+def test_op_type_matrix_host_validation():
+    L = mpigx.lib()
+    m = op_type_matrix()
+    for key, cls in m.items():
+        dt, op = key.split("/")
+        assert L.mpigx_op_valid(M.DTYPES[dt][0], M.OPS[op]) == cls, key
+    # bf16 extension: like FLOAT
+    for op in M.OPS:
+        assert L.mpigx_op_valid(C.MPIGX_BFLOAT16, M.OPS[op]) == M.op_valid("BFLOAT16", op)
+    assert L.mpigx_op_valid(12345, C.MPI_SUM) == C.MPI_ERR_TYPE
+    assert L.mpigx_op_valid(C.MPI_FLOAT, 777) == C.MPI_ERR_OP
+
+
+def test_type_sizes():
+    L = mpigx.lib()
+    sz = ctypes.c_int()
+    for name, (handle, npdt, _) in M.DTYPES.items():
+        assert L.mpigx_type_size(handle, ctypes.byref(sz)) == 0
+        import numpy as np
+        assert sz.value == np.dtype(npdt).itemsize, name
+    assert L.mpigx_type_size(1, ctypes.byref(sz)) == C.MPI_ERR_TYPE
+
+
+def test_error_strings_and_null_comm():
+    assert "Invalid MPI_Op" in mpigx.error_string(C.MPI_ERR_OP)
+    L = mpigx.lib()
+    # a NULL communicator is rejected before any device work
+    assert L.mpigx_allreduce(None, None, 1, C.MPI_FLOAT, C.MPI_SUM, None) == C.MPI_ERR_COMM
+    assert L.mpigx_barrier(None) == C.MPI_ERR_COMM
+    uid = mpigx._lib.UniqueId()
+    assert L.mpigx_get_unique_id(ctypes.byref(uid)) == 0
+    raw = ctypes.string_at(ctypes.addressof(uid), 128)
+    assert raw.startswith(b"/mpigx-")
+
+
+def test_python_mirror_op_mapping():
+    """operators.jl:39-45: Julia functions -> built-in ops; others are user ops."""
+    import operator
+
+    import torch
+    assert mpigx.Op(operator.add, torch.float32).val == C.MPI_SUM
+    assert mpigx.Op(operator.mul, torch.complex64).val == C.MPI_PROD
+    assert mpigx.Op(max, torch.int32).val == C.MPI_MAX
+    assert mpigx.Op(min, float).val == C.MPI_MIN
+    assert mpigx.Op(operator.and_, torch.int64).val == C.MPI_BAND
+    assert mpigx.Op(operator.xor, torch.uint8).val == C.MPI_BXOR
+    # & on floats is not a built-in (operators.jl:43-45 restricts to integers)
+    assert mpigx.Op(operator.and_, torch.float32).val is None
+    u = mpigx.Op(lambda x, y: 2 * x + y - x, torch.int64)
+    assert u.val is None and u.fn is not None
+
+
+def test_python_mirror_datatypes():
+    """datatypes.jl:29-60 + the by-size mapping of other primitives (:281-284)."""
+    import torch
+    D = mpigx.Datatype
+    assert D(torch.float32).val == C.MPI_FLOAT
+    assert D(torch.float64).val == C.MPI_DOUBLE
+    assert D(torch.int64).val == C.MPI_INT64_T
+    assert D(torch.complex128).val == C.MPI_C_DOUBLE_COMPLEX
+    assert D(torch.bfloat16).val == C.MPIGX_BFLOAT16
+    assert D(torch.float16).val == C.MPI_UINT16_T
+    assert D(torch.bool).val == C.MPI_UINT8_T
+    assert D(int).val == C.MPI_INT64_T
+    with pytest.raises(TypeError):
+        D(str)
