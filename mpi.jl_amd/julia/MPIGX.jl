@@ -1,0 +1,182 @@
+# MPIGX.jl — the MPI.jl side of the drop-in: device-resident buffers go to
+# libmpigx.so (MI355X engine) through ccall; everything else keeps going to
+# libmpi exactly as before.
+#
+# Load after MPI.jl:   using MPI; include("mpi.jl_amd/julia/MPIGX.jl"); using .MPIGX
+#
+# Plug points used (the only extension hooks MPI.jl offers, SURVEY.md §8b):
+#   * a device buffer type + Base.cconvert/unsafe_convert(::Type{MPIPtr}, ...)
+#     (src/buffers.jl:13-23, the role src/cuda.jl:6-24 plays for CuArray);
+#   * Datatype(T) for BFloat16 (src/datatypes.jl:269-292);
+#   * multiple dispatch on the collective signatures of src/collective.jl —
+#     the methods below have the reference's argument lists and differ only in
+#     the ccall target (:mpigx_* in libmpigx instead of :MPI_* in libmpi).
+# Julia is not installed in the build image, so this file is untested here;
+# the Python mirror (mpi.jl_amd/mpigx) exercises the same C ABI.
+module MPIGX
+
+using MPI
+import MPI: Comm, Op, Datatype, MPIPtr, SentinelPtr, MPI_Op, MPI_Datatype, @mpichk,
+            Allreduce!, Reduce!, Bcast!, Allgather!, Alltoall!, Scan!, Exscan!
+
+const libmpigx = get(ENV, "MPIGX_LIB", joinpath(@__DIR__, "..", "lib", "libmpigx.so"))
+const MPIGX_BFLOAT16 = Cint(1275068912)
+const IN_PLACE_PTR = Ptr{Cvoid}(-1 % UInt)
+
+# ---------------------------------------------------------------------------
+# device buffer (north-star subsystem 1): HBM allocation owned by Julia
+# ---------------------------------------------------------------------------
+mutable struct ROCBuffer{T,N} <: AbstractArray{T,N}
+    ptr::Ptr{T}
+    dims::NTuple{N,Int}
+    function ROCBuffer{T,N}(::UndefInitializer, dims::NTuple{N,Int}) where {T,N}
+        p = Ref{Ptr{Cvoid}}(C_NULL)
+        @mpichk ccall((:mpigx_malloc, libmpigx), Cint, (Ptr{Ptr{Cvoid}}, Csize_t), p, max(1, prod(dims)) * sizeof(T))
+        b = new{T,N}(Ptr{T}(p[]), dims)
+        finalizer(x -> ccall((:mpigx_free, libmpigx), Cint, (Ptr{Cvoid},), x.ptr), b)
+        return b
+    end
+end
+ROCBuffer{T}(::UndefInitializer, dims::Integer...) where {T} = ROCBuffer{T,length(dims)}(undef, Tuple(Int.(dims)))
+function ROCBuffer(a::Array{T,N}) where {T,N}
+    b = ROCBuffer{T,N}(undef, size(a))
+    ccall((:mpigx_memcpy, libmpigx), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t), b.ptr, a, sizeof(a))
+    return b
+end
+Base.size(b::ROCBuffer) = b.dims
+Base.similar(b::ROCBuffer{T}, ::Type{S}, dims::Dims) where {T,S} = ROCBuffer{S,length(dims)}(undef, dims)
+function Base.Array(b::ROCBuffer{T,N}) where {T,N}
+    a = Array{T,N}(undef, b.dims)
+    ccall((:mpigx_memcpy, libmpigx), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t), a, b.ptr, sizeof(a))
+    return a
+end
+Base.getindex(b::ROCBuffer, i::Int) = Array(b)[i]          # host copy; tests only
+Base.:(==)(a::ROCBuffer, b::AbstractArray) = Array(a) == b
+Base.cconvert(::Type{MPIPtr}, b::ROCBuffer) = b
+Base.unsafe_convert(::Type{MPIPtr}, b::ROCBuffer) = reinterpret(MPIPtr, b.ptr)
+
+const DeviceBuf = ROCBuffer
+const DeviceOrSentinel = Union{ROCBuffer,SentinelPtr}
+
+# ---------------------------------------------------------------------------
+# engine communicators, created collectively on first device use of a Comm;
+# the 128-byte unique id travels over host MPI (MPI.Bcast!)
+# ---------------------------------------------------------------------------
+const ENGINE = Dict{Cint,Ptr{Cvoid}}()
+
+function engine(comm::Comm)
+    get!(ENGINE, comm.val) do
+        id = zeros(UInt8, 128)
+        rank = MPI.Comm_rank(comm)
+        if rank == 0
+            @mpichk ccall((:mpigx_get_unique_id, libmpigx), Cint, (Ptr{UInt8},), id)
+        end
+        MPI.Bcast!(id, 0, comm)
+        # rank -> GPU binding: node-local rank (comm.jl:107 Comm_split_type SHARED)
+        local_comm = MPI.Comm_split_type(comm, MPI.MPI_COMM_TYPE_SHARED, rank)
+        device = parse(Int, get(ENV, "MPIGX_DEVICE", string(MPI.Comm_rank(local_comm))))
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        @mpichk ccall((:mpigx_comm_init_rank, libmpigx), Cint, (Ptr{Ptr{Cvoid}}, Cint, Ptr{UInt8}, Cint, Cint),
+                      h, MPI.Comm_size(comm), id, rank, device)
+        MPI.refcount_inc()  # freed (collectively) before MPI_Finalize
+        h[]
+    end
+end
+
+# ---------------------------------------------------------------------------
+# datatype extension (datatypes.jl:281-284 would map BFloat16 to UINT16_T)
+# ---------------------------------------------------------------------------
+if isdefined(Main, :BFloat16s)
+    Datatype(::Type{Main.BFloat16s.BFloat16}; commit=true) = MPI._Datatype(MPIGX_BFLOAT16)
+end
+
+# ---------------------------------------------------------------------------
+# collectives: the reference signatures, ccall target swapped
+# ---------------------------------------------------------------------------
+# collective.jl:29-37
+function Bcast!(buffer::ROCBuffer, count::Integer, root::Integer, comm::Comm)
+    @mpichk ccall((:mpigx_bcast, libmpigx), Cint, (MPIPtr, Cint, MPI_Datatype, Cint, Ptr{Cvoid}),
+                  buffer, count, Datatype(eltype(buffer)), root, engine(comm))
+    buffer
+end
+
+# collective.jl:295-307
+function Allgather!(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Integer, comm::Comm)
+    MPI.@assert_minlength recvbuf count*MPI.Comm_size(comm)
+    MPI.@assert_minlength sendbuf count
+    T = eltype(recvbuf)
+    @mpichk ccall((:mpigx_allgather, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, MPIPtr, Cint, MPI_Datatype, Ptr{Cvoid}),
+                  sendbuf, count, Datatype(T), recvbuf, count, Datatype(T), engine(comm))
+    recvbuf
+end
+
+# collective.jl:489-501
+function Alltoall!(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Integer, comm::Comm)
+    buflength = count * MPI.Comm_size(comm)
+    MPI.@assert_minlength recvbuf buflength
+    MPI.@assert_minlength sendbuf buflength
+    sendbuf isa SentinelPtr || @assert eltype(sendbuf) == eltype(recvbuf)
+    T = eltype(recvbuf)
+    @mpichk ccall((:mpigx_alltoall, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, MPIPtr, Cint, MPI_Datatype, Ptr{Cvoid}),
+                  sendbuf, count, Datatype(T), recvbuf, count, Datatype(T), engine(comm))
+    recvbuf
+end
+
+# collective.jl:605-618 (recvbuf may be `nothing` on non-roots)
+function Reduce!(sendbuf::DeviceOrSentinel, recvbuf::Union{ROCBuffer,Nothing}, count::Integer,
+                 op::Union{Op,MPI_Op}, root::Integer, comm::Comm)
+    isroot = MPI.Comm_rank(comm) == root
+    MPI.@assert_minlength sendbuf count
+    if isroot
+        @assert recvbuf !== nothing
+        MPI.@assert_minlength recvbuf count
+    end
+    T = sendbuf isa SentinelPtr ? eltype(recvbuf) : eltype(sendbuf)
+    @mpichk ccall((:mpigx_reduce, libmpigx), Cint,
+                  (MPIPtr, MPIPtr, Cint, MPI_Datatype, MPI_Op, Cint, Ptr{Cvoid}),
+                  sendbuf, recvbuf, count, Datatype(T), op, root, engine(comm))
+    recvbuf
+end
+
+# collective.jl:691-701
+function Allreduce!(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Integer,
+                    op::Union{Op,MPI_Op}, comm::Comm)
+    MPI.@assert_minlength sendbuf count
+    MPI.@assert_minlength recvbuf count
+    sendbuf isa SentinelPtr || @assert eltype(sendbuf) == eltype(recvbuf)
+    T = eltype(recvbuf)
+    @mpichk ccall((:mpigx_allreduce, libmpigx), Cint,
+                  (MPIPtr, MPIPtr, Cint, MPI_Datatype, MPI_Op, Ptr{Cvoid}),
+                  sendbuf, recvbuf, count, Datatype(T), op, engine(comm))
+    recvbuf
+end
+
+# collective.jl:760-768 / :834-842
+for (jl, c) in ((:Scan!, :mpigx_scan), (:Exscan!, :mpigx_exscan))
+    @eval function $jl(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Integer,
+                       op::Union{Op,MPI_Op}, comm::Comm)
+        T = eltype(recvbuf)
+        @mpichk ccall(($(QuoteNode(c)), libmpigx), Cint,
+                      (MPIPtr, MPIPtr, Cint, MPI_Datatype, MPI_Op, Ptr{Cvoid}),
+                      sendbuf, recvbuf, count, Datatype(T), op, engine(comm))
+        recvbuf
+    end
+end
+
+function __finalize()
+    for h in values(ENGINE)
+        ccall((:mpigx_comm_free, libmpigx), Cint, (Ptr{Cvoid},), h)
+        MPI.refcount_dec()
+    end
+    empty!(ENGINE)
+end
+# MPI.jl 0.14 has init hooks but no finalize hooks (environment.jl:26-62):
+# engine communicators hold a refcount like any MPI object, so the libmpi
+# finalizer runs after them (environment.jl:37-62, refcount_inc/_dec).
+atexit(__finalize)
+
+export ROCBuffer
+
+end # module
