@@ -1,12 +1,12 @@
-"""MPI.jl's collective API surface, over libmpigx, for device-resident buffers.
+"""MPI.jl's collective API surface: device buffers -> libmpigx, host -> libmpi.
 
-This is the host-side mirror of the reference's plugin point: Julia is absent
+This is the host-side mirror of the reference's plugin point.  Julia is absent
 from this image, so the MPI.jl wrappers that north_star keeps (src/comm.jl,
 src/buffers.jl, src/datatypes.jl, src/operators.jl, src/collective.jl) are
-restated here in Python with the same names (`!` becomes a trailing `_`),
-the same argument meaning, defaults and error behaviour:
+restated in Python with the same names (`!` becomes a trailing `_`), the same
+argument meaning, defaults and error behaviour:
 
-* argument checks are the reference's `@assert_minlength` /`@assert`
+* argument checks are the reference's `@assert_minlength` / `@assert`
   (buffers.jl:25-31) and raise ``AssertionError``;
 * non-zero return codes raise :class:`MPIError` like ``@mpichk``
   (error.jl:5-8);
@@ -14,9 +14,12 @@ the same argument meaning, defaults and error behaviour:
   allocating/scalar forms follow collective.jl line by line (cited per
   function).
 
-Device buffers are torch tensors on a ROCm device (the ``ROCBuffer`` role of
-SURVEY.md §7 step 7); the bytes never leave HBM.  The Julia ccall glue that
-does the same for MPI.jl is mpi.jl_amd/julia/MPIGX.jl.
+Dispatch is the one MPI.jl performs with CuArrays (src/cuda.jl): device
+buffers (torch tensors on a ROCm device — the ``ROCBuffer`` role of SURVEY.md
+§7 step 7) go to ``mpigx_<coll>`` in libmpigx.so; host numpy arrays keep going
+to ``MPI_<Coll>`` in libmpi (hostmpi.py).  Both receive the *same* argument
+list — that identity is the drop-in boundary.  The Julia glue that does the
+same for MPI.jl is mpi.jl_amd/julia/MPIGX.jl (INTEGRATION.md).
 """
 from __future__ import annotations
 
@@ -25,7 +28,10 @@ import operator
 import os
 import time
 
+import numpy as np
+
 from . import consts as C
+from . import hostmpi
 from ._lib import UniqueId, lib
 
 IN_PLACE = object()  # MPI_IN_PLACE sentinel (consts_mpich.jl:105)
@@ -91,6 +97,8 @@ FLOAT, DOUBLE = _mk("FLOAT", C.MPI_FLOAT), _mk("DOUBLE", C.MPI_DOUBLE)
 C_FLOAT_COMPLEX, C_DOUBLE_COMPLEX = _mk("C_FLOAT_COMPLEX", C.MPI_C_FLOAT_COMPLEX), _mk(
     "C_DOUBLE_COMPLEX", C.MPI_C_DOUBLE_COMPLEX)
 BFLOAT16 = _mk("BFLOAT16", C.MPIGX_BFLOAT16)
+_BY_VAL = {d.val: d for d in (INT8_T, UINT8_T, INT16_T, UINT16_T, INT32_T, UINT32_T, INT64_T, UINT64_T, BYTE,
+                              CHAR, WCHAR, FLOAT, DOUBLE, C_FLOAT_COMPLEX, C_DOUBLE_COMPLEX, BFLOAT16)}
 
 
 def _torch():
@@ -99,12 +107,24 @@ def _torch():
 
 
 def _datatype_of(T) -> Datatype:
-    """Datatype(T) for torch dtypes / Python scalar types (datatypes.jl:29-60).
-
-    Unnamed 1/2/4/8-byte primitives go by size to UINT8/16/32/64_T exactly as
-    datatypes.jl:281-284 does (so float16 and bool are integer bit patterns,
-    as in the reference); bfloat16 gets mpigx's BFLOAT16 extension.
-    """
+    """Datatype(T) for torch / numpy dtypes and Python scalar types
+    (datatypes.jl:29-60).  Unnamed 1/2/4/8-byte primitives go by size to
+    UINT8/16/32/64_T exactly as datatypes.jl:281-284 does (so float16 and bool
+    are integer bit patterns, as in the reference); torch.bfloat16 gets the
+    BFLOAT16 extension."""
+    if T is int:
+        return INT64_T
+    if T is float:
+        return DOUBLE
+    if T is complex:
+        return C_DOUBLE_COMPLEX
+    if T is bool:
+        return UINT8_T
+    if isinstance(T, np.dtype) or (isinstance(T, type) and issubclass(T, np.generic)):
+        h = hostmpi.HANDLE_OF_NP.get(np.dtype(T))
+        if h is None:
+            raise TypeError(f"no MPI datatype for {T!r}")
+        return _BY_VAL[h]
     torch = _torch()
     table = {
         torch.int8: INT8_T, torch.uint8: UINT8_T, torch.int16: INT16_T, torch.int32: INT32_T,
@@ -117,14 +137,6 @@ def _datatype_of(T) -> Datatype:
             table[getattr(torch, nm)] = dt
     if T in table:
         return table[T]
-    if T is int:
-        return INT64_T
-    if T is float:
-        return DOUBLE
-    if T is complex:
-        return C_DOUBLE_COMPLEX
-    if T is bool:
-        return UINT8_T
     raise TypeError(f"no MPI datatype for {T!r}")
 
 
@@ -134,6 +146,8 @@ _COMPLEX = ("complex64", "complex128")
 
 
 def _kind(T) -> str:
+    if isinstance(T, np.dtype):
+        T = T.name
     name = str(T).replace("torch.", "")
     if T is int or name in _INTEGER:
         return "int"
@@ -213,7 +227,7 @@ def _as_op(op, T) -> Op:
 # Buffer (src/buffers.jl:78-127)
 # ---------------------------------------------------------------------------
 class Buffer:
-    """MPI.Buffer(data, count, datatype): device tensor + count + Datatype."""
+    """MPI.Buffer(data, count, datatype): array + count + Datatype."""
     __slots__ = ("data", "count", "datatype")
 
     def __init__(self, data, count=None, datatype=None):
@@ -221,8 +235,16 @@ class Buffer:
             self.data, self.count, self.datatype = data.data, data.count, data.datatype
             return
         self.data = data
-        self.count = int(count if count is not None else data.numel())
+        self.count = int(count if count is not None else _len(data))
         self.datatype = Datatype(datatype if datatype is not None else data.dtype)
+
+
+def _unwrap(buf):
+    return buf.data if isinstance(buf, Buffer) else buf
+
+
+def _is_host(buf):
+    return isinstance(_unwrap(buf), np.ndarray)
 
 
 def _ptr(buf):
@@ -230,19 +252,22 @@ def _ptr(buf):
         return None
     if buf is IN_PLACE:
         return _IN_PLACE_PTR
-    if isinstance(buf, Buffer):
-        buf = buf.data
-    if not getattr(buf, "is_cuda", False):
-        raise TypeError("mpigx handles device-resident buffers (ROCm tensors); host buffers stay on libmpi")
-    if not buf.is_contiguous():
+    b = _unwrap(buf)
+    if isinstance(b, np.ndarray):
+        if not b.flags.c_contiguous:
+            raise ValueError("non-contiguous buffers need derived datatypes (out of scope)")
+        return ctypes.c_void_p(b.ctypes.data)
+    if not getattr(b, "is_cuda", False):
+        raise TypeError("buffers must be numpy arrays (host, libmpi) or ROCm tensors (device, libmpigx)")
+    if not b.is_contiguous():
         raise ValueError("non-contiguous device buffers need derived datatypes (SURVEY.md §8f, out of scope)")
-    return ctypes.c_void_p(buf.data_ptr())
+    return ctypes.c_void_p(b.data_ptr())
 
 
 def _len(buf):
     if isinstance(buf, Buffer):
         return buf.count
-    return buf.numel()
+    return buf.size if isinstance(buf, np.ndarray) else buf.numel()
 
 
 def _eltype(buf):
@@ -258,24 +283,38 @@ def _assert_minlength(buf, count):
 
 
 def _is_array(x):
-    return hasattr(x, "numel") or isinstance(x, Buffer)
+    return isinstance(x, (np.ndarray, Buffer)) or hasattr(x, "numel")
+
+
+def _empty_like(buf, count=None):
+    b = _unwrap(buf)
+    if isinstance(b, np.ndarray):
+        return np.empty(b.shape if count is None else (count,), dtype=b.dtype)
+    torch = _torch()
+    return torch.empty_like(b) if count is None else torch.empty(count, dtype=b.dtype, device=b.device)
+
+
+def _dtype(buf):
+    return getattr(_unwrap(buf), "dtype", None)
 
 
 # ---------------------------------------------------------------------------
 # Comm (src/comm.jl) + environment (src/environment.jl)
 # ---------------------------------------------------------------------------
 class Comm:
-    __slots__ = ("val", "_rank", "_size", "device")
+    """`val` = libmpigx communicator (device buffers), `host` = libmpi MPI_Comm
+    handle (host buffers); either may be None."""
+    __slots__ = ("val", "host", "_rank", "_size", "device")
 
-    def __init__(self, handle, rank, size, device):
-        self.val, self._rank, self._size, self.device = handle, rank, size, device
+    def __init__(self, handle, rank, size, device, host=None):
+        self.val, self._rank, self._size, self.device, self.host = handle, rank, size, device, host
 
     def __repr__(self):
         return f"MPI.Comm(rank={self._rank}, size={self._size}, device={self.device})"
 
 
 COMM_WORLD = None
-_state = {"init": False, "final": False, "pg_owned": False}
+_state = {"init": False, "final": False, "pg_owned": False, "host": False}
 
 
 def _env_int(*names, default=None):
@@ -286,47 +325,64 @@ def _env_int(*names, default=None):
     return default
 
 
-def _bootstrap_id(rank, size):
-    """Distribute rank 0's mpigx unique id (the role MPI_Bcast plays for the
-    Julia glue)."""
+def _bootstrap_id(rank, size, host_comm=None):
+    """Distribute rank 0's mpigx unique id: host MPI_Bcast when libmpi is up
+    (what the Julia glue does), else torch.distributed (gloo)."""
     uid = UniqueId()
     if rank == 0:
         _check(lib().mpigx_get_unique_id(ctypes.byref(uid)))
     if size == 1:
         return uid
-    import torch.distributed as dist
-    if not dist.is_initialized():
-        dist.init_process_group("gloo", rank=rank, world_size=size)
-        _state["pg_owned"] = True
-    obj = [ctypes.string_at(ctypes.addressof(uid), 128) if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0)
-    ctypes.memmove(ctypes.addressof(uid), bytes(obj[0]), 128)
+    raw = ctypes.string_at(ctypes.addressof(uid), 128)
+    if host_comm is not None:
+        raw = hostmpi.bcast_bytes(raw, 0, host_comm)
+    else:
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            dist.init_process_group("gloo", rank=rank, world_size=size)
+            _state["pg_owned"] = True
+        obj = [raw if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        raw = obj[0]
+    ctypes.memmove(ctypes.addressof(uid), bytes(raw), 128)
     return uid
 
 
 def Init(threadlevel=None):
     """environment.jl:80: Init binds this rank to its GPU and builds COMM_WORLD.
 
-    Rank/size come from the launcher (torchrun RANK/WORLD_SIZE/LOCAL_RANK or
-    hydra PMI_RANK/PMI_SIZE/MPI_LOCALRANKID); device = MPIGX_DEVICE or
-    local_rank mod visible devices (comm.jl:107 Comm_split_type(SHARED)).
+    Rank/size come from the launcher (hydra/mpiexec PMI_RANK/PMI_SIZE, which
+    also brings up host libmpi, or torchrun RANK/WORLD_SIZE/LOCAL_RANK);
+    device = MPIGX_DEVICE or the node-local rank mod visible devices
+    (comm.jl:107 Comm_split_type(SHARED)).  Without a ROCm device (or with
+    MPIGX_HOST_ONLY=1) only the host (libmpi) side exists.
     """
     global COMM_WORLD
     if _state["init"]:
         raise AssertionError("MPI.Init called twice")
-    torch = _torch()
-    rank = _env_int("RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", default=0)
-    size = _env_int("WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", default=1)
+    host = None
+    if hostmpi.available():
+        rank, size = hostmpi.init()
+        host = C.MPI_COMM_WORLD
+        _state["host"] = True
+    else:
+        rank = _env_int("RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", default=0)
+        size = _env_int("WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", default=1)
     local = _env_int("LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", default=rank)
-    ndev = torch.cuda.device_count()
-    if ndev == 0:
-        raise RuntimeError("mpigx: no ROCm device visible")
-    device = _env_int("MPIGX_DEVICE", default=local % ndev)
-    torch.cuda.set_device(device)
-    uid = _bootstrap_id(rank, size)
-    h = ctypes.c_void_p()
-    _check(lib().mpigx_comm_init_rank(ctypes.byref(h), size, ctypes.byref(uid), rank, device))
-    COMM_WORLD = Comm(h, rank, size, device)
+    ndev = 0
+    if os.environ.get("MPIGX_HOST_ONLY") != "1":
+        ndev = _torch().cuda.device_count()
+    handle, device = None, None
+    if ndev > 0:
+        device = _env_int("MPIGX_DEVICE", default=local % ndev)
+        _torch().cuda.set_device(device)
+        uid = _bootstrap_id(rank, size, host)
+        h = ctypes.c_void_p()
+        _check(lib().mpigx_comm_init_rank(ctypes.byref(h), size, ctypes.byref(uid), rank, device))
+        handle = h
+    elif host is None:
+        raise RuntimeError("mpigx: no ROCm device and no host libmpi (start under mpiexec for host buffers)")
+    COMM_WORLD = Comm(handle, rank, size, device, host)
     _state["init"] = True
     return COMM_WORLD
 
@@ -341,13 +397,15 @@ def Finalized():
 
 def Finalize():
     global COMM_WORLD
-    if COMM_WORLD is not None:
+    if COMM_WORLD is not None and COMM_WORLD.val:
         _check(lib().mpigx_comm_free(COMM_WORLD.val))
-        COMM_WORLD = None
+    COMM_WORLD = None
     if _state["pg_owned"]:
         import torch.distributed as dist
         dist.destroy_process_group()
         _state["pg_owned"] = False
+    if _state["host"]:
+        hostmpi.finalize()
     _state["final"] = True
 
 
@@ -374,19 +432,24 @@ def Comm_size(comm: Comm) -> int:
 
 def Comm_dup(comm: Comm) -> Comm:
     """comm.jl:78: a new communicator over the same ranks (own arenas/epochs).
-
-    Its unique id is broadcast over `comm` itself, through the device engine.
-    """
-    torch = _torch()
+    The unique id is broadcast over `comm` itself (host libmpi, or the engine)."""
     uid = UniqueId()
     if comm._rank == 0:
         _check(lib().mpigx_get_unique_id(ctypes.byref(uid)))
-    t = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(uid), 128)), dtype=torch.uint8).to(f"cuda:{comm.device}")
-    Bcast_(t, 0, comm)
-    ctypes.memmove(ctypes.addressof(uid), bytes(t.cpu().numpy().tobytes()), 128)
-    h = ctypes.c_void_p()
-    _check(lib().mpigx_comm_init_rank(ctypes.byref(h), comm._size, ctypes.byref(uid), comm._rank, comm.device))
-    return Comm(h, comm._rank, comm._size, comm.device)
+    raw = ctypes.string_at(ctypes.addressof(uid), 128)
+    if comm.host is not None:
+        raw = hostmpi.bcast_bytes(raw, 0, comm.host)
+    elif comm.val:
+        torch = _torch()
+        t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(f"cuda:{comm.device}")
+        Bcast_(t, 0, comm)
+        raw = bytes(t.cpu().numpy().tobytes())
+    ctypes.memmove(ctypes.addressof(uid), raw, 128)
+    h = None
+    if comm.val:
+        h = ctypes.c_void_p()
+        _check(lib().mpigx_comm_init_rank(ctypes.byref(h), comm._size, ctypes.byref(uid), comm._rank, comm.device))
+    return Comm(h, comm._rank, comm._size, comm.device, comm.host)
 
 
 def Comm_split_type(comm: Comm, split_type, key, info=None) -> Comm:
@@ -413,13 +476,38 @@ def _stream(comm):
     lib().mpigx_comm_set_stream(comm.val, ctypes.c_void_p(s))
 
 
+def _call(coll, buf, comm, *args):
+    """One ccall: `MPI_<coll>` in libmpi for host buffers, `mpigx_<coll>` in
+    libmpigx for device buffers — the same argument list either way."""
+    if _is_host(buf):
+        if comm.host is None:
+            raise TypeError("host buffers need host libmpi (start the ranks with mpiexec)")
+        rc = getattr(hostmpi.lib(), "MPI_" + coll)(*args, comm.host)
+    else:
+        if not comm.val:
+            raise TypeError("device buffers need a ROCm device")
+        _stream(comm)
+        rc = getattr(lib(), "mpigx_" + coll.lower())(*args, comm.val)
+    _check(rc)
+
+
+def _op_val(opx, buf):
+    """Built-in handle, or (host only) an MPI_Op_create'd user function."""
+    if opx.val is not None:
+        return opx.val
+    return hostmpi.user_op(opx.fn, _unwrap(buf).dtype, opx.iscommutative)
+
+
 # ---------------------------------------------------------------------------
 # collectives (src/collective.jl)
 # ---------------------------------------------------------------------------
 def Barrier(comm: Comm):
-    """collective.jl:15-19."""
-    _stream(comm)
-    _check(lib().mpigx_barrier(comm.val))
+    """collective.jl:15-19 (device engine barrier when a device exists)."""
+    if comm.val:
+        _stream(comm)
+        _check(lib().mpigx_barrier(comm.val))
+    if comm.host is not None:
+        _check(hostmpi.lib().MPI_Barrier(comm.host))
 
 
 def Bcast_(buf, *args):
@@ -429,8 +517,7 @@ def Bcast_(buf, *args):
     else:
         root, comm = args
         count = _len(buf)
-    _stream(comm)
-    _check(lib().mpigx_bcast(_ptr(buf), int(count), _eltype(buf).val, int(root), comm.val))
+    _call("Bcast", buf, comm, _ptr(buf), int(count), _eltype(buf).val, int(root))
     return buf
 
 
@@ -445,25 +532,22 @@ def Allgather_(*args):
     _assert_minlength(recvbuf, count * Comm_size(comm))
     _assert_minlength(sendbuf, count)
     T = _eltype(recvbuf)
-    _stream(comm)
-    _check(lib().mpigx_allgather(_ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val, comm.val))
+    _call("Allgather", recvbuf, comm, _ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val)
     return recvbuf
 
 
 def Allgather(*args):
     """Allgather(sendbuf[, count], comm) / Allgather(obj, comm) — collective.jl:327-335."""
-    torch = _torch()
     if len(args) == 3:
         sendbuf, count, comm = args
-        return Allgather_(sendbuf, torch.empty(Comm_size(comm) * count, dtype=sendbuf.dtype,
-                                               device=sendbuf.device), count, comm)
+        return Allgather_(sendbuf, _empty_like(sendbuf, Comm_size(comm) * count), count, comm)
     sendbuf, comm = args
     if _is_array(sendbuf):
         return Allgather(sendbuf, _len(sendbuf), comm)
     ref = _scalar_ref(sendbuf, comm)
-    out = torch.empty(Comm_size(comm), dtype=ref.dtype, device=ref.device)
+    out = _empty_like(ref, Comm_size(comm))
     Allgather_(ref, out, 1, comm)
-    return out.cpu().tolist()
+    return (out if isinstance(out, np.ndarray) else out.cpu().numpy()).tolist()
 
 
 def Alltoall_(*args):
@@ -480,35 +564,36 @@ def Alltoall_(*args):
     if sendbuf is not IN_PLACE:
         assert _eltype(sendbuf) == _eltype(recvbuf)
     T = _eltype(recvbuf)
-    _stream(comm)
-    _check(lib().mpigx_alltoall(_ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val, comm.val))
+    _call("Alltoall", recvbuf, comm, _ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val)
     return recvbuf
 
 
 def Alltoall(sendbuf, count, comm):
     """collective.jl:529-532."""
-    torch = _torch()
-    recvbuf = torch.empty(Comm_size(comm) * count, dtype=sendbuf.dtype, device=sendbuf.device)
-    return Alltoall_(sendbuf, recvbuf, count, comm)
+    return Alltoall_(sendbuf, _empty_like(sendbuf, Comm_size(comm) * count), count, comm)
 
 
 def _scalar_ref(obj, comm):
-    """`Ref(object)` of the scalar forms, as a 1-element device tensor."""
-    torch = _torch()
-    if isinstance(obj, bool):
-        dt = torch.uint8
-    elif isinstance(obj, int):
-        dt = torch.int64
-    elif isinstance(obj, float):
-        dt = torch.float64
-    elif isinstance(obj, complex):
-        dt = torch.complex128
-    elif hasattr(obj, "dtype") and hasattr(obj, "item"):
-        dt = obj.dtype
-        obj = obj.item()
+    """`Ref(object)` of the scalar forms: a 1-element host array when host
+    libmpi is up (as in MPI.jl), else a 1-element device tensor."""
+    if isinstance(obj, (bool, np.bool_)):
+        npdt = np.uint8
+    elif isinstance(obj, (int, np.integer)):
+        npdt = np.int64 if isinstance(obj, int) else obj.dtype
+    elif isinstance(obj, (float, np.floating)):
+        npdt = np.float64 if isinstance(obj, float) else obj.dtype
+    elif isinstance(obj, (complex, np.complexfloating)):
+        npdt = np.complex128 if isinstance(obj, complex) else obj.dtype
     else:
         raise TypeError(f"unsupported scalar {obj!r}")
-    return torch.tensor([obj], dtype=dt, device=f"cuda:{comm.device}")
+    a = np.array([obj], dtype=npdt)
+    if comm.host is not None:
+        return a
+    return _torch().from_numpy(a).to(f"cuda:{comm.device}")
+
+
+def _item(x):
+    return x[0].item() if isinstance(x, np.ndarray) else x.item()
 
 
 def _user_fold(xs, fn):
@@ -562,34 +647,27 @@ def Reduce_(*args):
     if isroot:
         assert recvbuf is not None
         _assert_minlength(recvbuf, count)
-    T = _eltype(recvbuf) if sendbuf is IN_PLACE else _eltype(sendbuf)
-    opx = _as_op(op, _torch_dtype(sendbuf if sendbuf is not IN_PLACE else recvbuf))
-    if opx.val is None:
+    data = recvbuf if sendbuf is IN_PLACE else sendbuf
+    T = _eltype(data)
+    opx = _as_op(op, _dtype(data))
+    if opx.val is None and not _is_host(data):
         return _user_collective("reduce", sendbuf, recvbuf, count, opx, root, comm)
-    _stream(comm)
-    _check(lib().mpigx_reduce(_ptr(sendbuf), _ptr(recvbuf), int(count), T.val, opx.val, int(root), comm.val))
+    _call("Reduce", data, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val, _op_val(opx, data), int(root))
     return recvbuf
 
 
 def Reduce(sendbuf, op, root, comm):
     """collective.jl:657-666: allocating; `nothing` (None) on non-roots."""
-    torch = _torch()
     if _is_array(sendbuf):
-        recv = torch.empty_like(sendbuf) if Comm_rank(comm) == root else None
+        recv = _empty_like(sendbuf) if Comm_rank(comm) == root else None
         return Reduce_(sendbuf, recv, _len(sendbuf), op, root, comm)
     ref = _scalar_ref(sendbuf, comm)
     if Comm_rank(comm) == root:
-        out = torch.empty_like(ref)
+        out = _empty_like(ref)
         Reduce_(ref, out, 1, op, root, comm)
-        return out.item()
+        return _item(out)
     Reduce_(ref, None, 1, op, root, comm)
     return None
-
-
-def _torch_dtype(buf):
-    if isinstance(buf, Buffer):
-        buf = buf.data
-    return getattr(buf, "dtype", None)
 
 
 def Allreduce_(*args):
@@ -608,26 +686,24 @@ def Allreduce_(*args):
     if sendbuf is not IN_PLACE:
         assert _eltype(sendbuf) == _eltype(recvbuf)
     T = _eltype(recvbuf)
-    opx = _as_op(op, _torch_dtype(recvbuf))
-    if opx.val is None:
+    opx = _as_op(op, _dtype(recvbuf))
+    if opx.val is None and not _is_host(recvbuf):
         return _user_collective("allreduce", sendbuf, recvbuf, count, opx, 0, comm)
-    _stream(comm)
-    _check(lib().mpigx_allreduce(_ptr(sendbuf), _ptr(recvbuf), int(count), T.val, opx.val, comm.val))
+    _call("Allreduce", recvbuf, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val, _op_val(opx, recvbuf))
     return recvbuf
 
 
 def Allreduce(sendbuf, op, comm):
     """collective.jl:733-738: allocating (`similar`) or scalar (`Ref`) form."""
-    torch = _torch()
     if _is_array(sendbuf):
-        return Allreduce_(sendbuf, torch.empty_like(sendbuf), _len(sendbuf), op, comm)
+        return Allreduce_(sendbuf, _empty_like(sendbuf), _len(sendbuf), op, comm)
     ref = _scalar_ref(sendbuf, comm)
-    out = torch.empty_like(ref)
+    out = _empty_like(ref)
     Allreduce_(ref, out, 1, op, comm)
-    return out.item()
+    return _item(out)
 
 
-def _scan_dispatch(args, name):
+def _scan_dispatch(args):
     """Scan!/Exscan!(sendbuf, recvbuf, count, op, comm) | (sendbuf, recvbuf, op, comm)
     | in-place (buf, count, op, comm) | (buf, op, comm).  (collective.jl:760-783 /
     :834-857 — the reference's in-place forms use an undefined `sendbuf`; here
@@ -644,14 +720,13 @@ def _scan_dispatch(args, name):
 
 
 def _scan_common(args, exclusive):
-    sendbuf, recvbuf, count, op, comm = _scan_dispatch(args, "Exscan!" if exclusive else "Scan!")
+    sendbuf, recvbuf, count, op, comm = _scan_dispatch(args)
     T = _eltype(recvbuf)
-    opx = _as_op(op, _torch_dtype(recvbuf))
-    if opx.val is None:
+    opx = _as_op(op, _dtype(recvbuf))
+    if opx.val is None and not _is_host(recvbuf):
         return _user_collective("exscan" if exclusive else "scan", sendbuf, recvbuf, count, opx, 0, comm)
-    _stream(comm)
-    f = lib().mpigx_exscan if exclusive else lib().mpigx_scan
-    _check(f(_ptr(sendbuf), _ptr(recvbuf), int(count), T.val, opx.val, comm.val))
+    _call("Exscan" if exclusive else "Scan", recvbuf, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val,
+          _op_val(opx, recvbuf))
     return recvbuf
 
 
@@ -667,24 +742,22 @@ def Exscan_(*args):
 
 def Scan(sendbuf, op, comm):
     """collective.jl:803-808."""
-    torch = _torch()
     if _is_array(sendbuf):
-        return Scan_(sendbuf, torch.empty_like(sendbuf), op, comm)
+        return Scan_(sendbuf, _empty_like(sendbuf), op, comm)
     ref = _scalar_ref(sendbuf, comm)
-    out = torch.empty_like(ref)
+    out = _empty_like(ref)
     Scan_(ref, out, 1, op, comm)
-    return out.item()
+    return _item(out)
 
 
 def Exscan(sendbuf, op, comm):
     """collective.jl:877-882 (rank 0's result is undefined: its buffer is untouched)."""
-    torch = _torch()
     if _is_array(sendbuf):
-        return Exscan_(sendbuf, torch.empty_like(sendbuf), op, comm)
+        return Exscan_(sendbuf, _empty_like(sendbuf), op, comm)
     ref = _scalar_ref(sendbuf, comm)
-    out = torch.zeros_like(ref)
+    out = ref * 0
     Exscan_(ref, out, 1, op, comm)
-    return out.item()
+    return _item(out)
 
 
 # ---------------------------------------------------------------------------
@@ -693,7 +766,7 @@ def Exscan(sendbuf, op, comm):
 def Reduce_local_(inbuf, inoutbuf, count, op):
     """MPI_Reduce_local (mpi.h:1357): inoutbuf = op(inoutbuf, inbuf)."""
     T = _eltype(inoutbuf)
-    opx = _as_op(op, _torch_dtype(inoutbuf))
+    opx = _as_op(op, _dtype(inoutbuf))
     _check(lib().mpigx_reduce_local(_ptr(inbuf), _ptr(inoutbuf), int(count), T.val, opx.val))
     return inoutbuf
 

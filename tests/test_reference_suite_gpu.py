@@ -1,0 +1,21 @@
+"""MPI.jl's collective test scripts (tests/spmd/ref_tests.py) in device mode —
+the equivalent of JULIA_MPI_TEST_ARRAYTYPE=CuArray (test_allreduce.jl:4-9):
+every buffer is a ROCm tensor and goes through libmpigx."""
+import json
+import os
+
+import pytest
+
+from spmd_launch import ROOT, launch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_reference_suite_device(n):
+    env = {"MPIGX_TEST_ARRAYTYPE": "ROCArray", "MPIGX_DEVICE": "0", "MPIGX_MAX_BLOCKS": "16",
+           "MPIGX_TIMEOUT_MS": "30000", "MPIGX_STAGING_BYTES": str(16 << 20)}
+    rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "ref_tests.py"), n, timeout=600, extra_env=env)
+    summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
+    assert all(rc == 0 for rc in rcs), "\n".join(o[-2000:] for o in outs)
+    assert len(summ) == n and all(s["nfail"] == 0 and s["device"] for s in summ), summ
