@@ -755,7 +755,7 @@ def Exscan(sendbuf, op, comm):
     if _is_array(sendbuf):
         return Exscan_(sendbuf, _empty_like(sendbuf), op, comm)
     ref = _scalar_ref(sendbuf, comm)
-    out = ref * 0
+    out = np.zeros_like(ref) if isinstance(ref, np.ndarray) else _torch().zeros_like(ref)
     Exscan_(ref, out, 1, op, comm)
     return _item(out)
 
