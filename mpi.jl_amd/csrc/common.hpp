@@ -85,7 +85,8 @@ struct CopyArgs {
   int root;
   long long bytes;     // bytes per rank contribution (bcast: whole buffer)
   long long slice;     // bytes per block slice (multiple of 16)
-  long long total;     // alltoall: per-destination block stride in bytes (=bytes)
+  long long total;     // user-buffer stride between rank blocks (bytes of one full block)
+  long long sstride;   // alltoall: staging stride between rank blocks (bytes rounded up to 16)
   const void* send;
   void* recv;
 };

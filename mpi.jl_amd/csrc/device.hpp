@@ -357,6 +357,48 @@ __device__ __forceinline__ void block_copy(char* dst, const char* src, long long
 }
 
 // ---------------------------------------------------------------------------
+// block-cooperative copy of up to NMAX (dst, src, len) pairs with the pairs
+// INTERLEAVED per thread: every iteration issues one 16-B load per pair
+// before storing, so when the sources are different peers every xGMI link
+// carries traffic at all times (a peer-by-peer loop would drive one link at
+// a time across the whole grid).  Falls back to per-pair block_copy when a
+// pair is not 16-B aligned.
+// ---------------------------------------------------------------------------
+template <int NMAX>
+__device__ __forceinline__ void block_gather(char* const (&dst)[NMAX], const char* const (&src)[NMAX],
+                                             const long long (&len)[NMAX], int m) {
+  bool vec = true;
+  long long nvmax = 0;
+#pragma unroll
+  for (int p = 0; p < NMAX; ++p)
+    if (p < m) {
+      vec &= ((((uintptr_t)dst[p]) | ((uintptr_t)src[p])) & 15) == 0;
+      const long long nv = len[p] / 16;
+      nvmax = nv > nvmax ? nv : nvmax;
+    }
+  if (!vec) {
+#pragma unroll
+    for (int p = 0; p < NMAX; ++p)
+      if (p < m) block_copy(dst[p], src[p], len[p]);
+    return;
+  }
+  const long long tid = threadIdx.x, nt = blockDim.x;
+  for (long long i = tid; i < nvmax; i += nt) {
+    u32x4 v[NMAX];
+#pragma unroll
+    for (int p = 0; p < NMAX; ++p)
+      if (p < m && i < len[p] / 16) v[p] = ld16(src[p] + 16 * i);
+#pragma unroll
+    for (int p = 0; p < NMAX; ++p)
+      if (p < m && i < len[p] / 16) st16(dst[p] + 16 * i, v[p]);
+  }
+#pragma unroll
+  for (int p = 0; p < NMAX; ++p)
+    if (p < m)
+      for (long long j = (len[p] / 16) * 16 + tid; j < len[p]; j += nt) dst[p][j] = src[p][j];
+}
+
+// ---------------------------------------------------------------------------
 // cross-rank barrier of block `blockIdx.x` on every rank, at epoch `ep`.
 // Producer side: every wave drains its stores, block barrier, one wave issues
 // a SYSTEM-scope release (writes this XCD's L2 back so peers reading our HBM

@@ -84,14 +84,26 @@ __global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
   (void)W;
   if (!rank_barrier(pv, ep++)) return;
   if (A.mode == M_AR_TWOSHOT || r == A.root) {
-    // allgather (or gather at root): every other rank's reduced chunk
-    for (int k = 1; k < n; ++k) {
-      const int p = (r + k) % n;  // stagger the peers so links load evenly
-      const long long c0 = lmin((long long)p * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
-      const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
-      const T* ps = (const T*)pv.stage[p];
-      block_copy((char*)(recv + lo), (const char*)(ps + lo), (hi - lo) * es);
+    // allgather (or gather at root): every other rank's reduced chunk,
+    // all peers interleaved per thread so every link is busy
+    char* dsts[NMAX];
+    const char* srcs[NMAX];
+    long long lens[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      dsts[j] = nullptr;
+      srcs[j] = nullptr;
+      lens[j] = 0;
+      if (j + 1 < n) {
+        const int p = (r + 1 + j) % n;
+        const long long c0 = lmin((long long)p * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+        const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+        dsts[j] = (char*)(recv + lo);
+        srcs[j] = (const char*)((const T*)pv.stage[p] + lo);
+        lens[j] = (hi - lo) * es;
+      }
     }
+    block_gather<NMAX>(dsts, srcs, lens, n - 1);
   }
   rank_barrier(pv, ep++);
 }
@@ -185,10 +197,5 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs A) {
   }
   rank_barrier(pv, ep++);
 }
-
-// ---------------------------------------------------------------------------
-// byte-movement collectives
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A);
 
 }  // namespace mpigx

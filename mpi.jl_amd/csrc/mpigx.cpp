@@ -721,6 +721,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
     a.mode = alltoall ? C_ALLTOALL : C_ALLGATHER;
     a.bytes = len;
     a.total = bytes;
+    a.sstride = rup(len, 16);
     const int g = grid_for(c, len * (alltoall ? n : 1));
     a.slice = rup(cdiv(len, g), 16);
     if (alltoall) {
