@@ -8,7 +8,16 @@
 namespace mpigx {
 
 template <int NMAX>
+__device__ __forceinline__ void copy_body(const CopyArgs& A);
+
+template <int NMAX>
 __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
+  copy_body<NMAX>(A);
+  signal_done(A.pv);
+}
+
+template <int NMAX>
+__device__ __forceinline__ void copy_body(const CopyArgs& A) {
   const PeerView& pv = A.pv;
   const int b = blockIdx.x, r = pv.rank, n = pv.n;
   uint64_t ep = pv.epoch;

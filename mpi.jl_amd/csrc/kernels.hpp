@@ -21,8 +21,27 @@ namespace mpigx {
 
 __device__ __forceinline__ long long lmin(long long a, long long b) { return a < b ? a : b; }
 
+// Completion signal for blocking calls: every block adds 1 to a host-mapped
+// counter after its last access (the host spins on it instead of paying a
+// hipStreamSynchronize round trip).
+__device__ __forceinline__ void signal_done(const PeerView& pv) {
+  if (pv.done) {
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(pv.done, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <class OP, class T, int NMAX, int SCHED>
+__device__ __forceinline__ void fold_body(const FoldArgs& A);
+
 template <class OP, class T, int NMAX, int SCHED>
 __global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
+  fold_body<OP, T, NMAX, SCHED>(A);
+  signal_done(A.pv);
+}
+
+template <class OP, class T, int NMAX, int SCHED>
+__device__ __forceinline__ void fold_body(const FoldArgs& A) {
   const T* const* src = reinterpret_cast<const T* const*>(A.src);
   const T* const* src2 = reinterpret_cast<const T* const*>(A.src2);
   const PeerView& pv = A.pv;
@@ -164,7 +183,16 @@ __device__ __forceinline__ void scan_at(const ScanArgs& A, long long e, T (&res)
 }
 
 template <class OP, class T>
+__device__ __forceinline__ void scan_body(const ScanArgs& A);
+
+template <class OP, class T>
 __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs A) {
+  scan_body<OP, T>(A);
+  signal_done(A.pv);
+}
+
+template <class OP, class T>
+__device__ __forceinline__ void scan_body(const ScanArgs& A) {
   constexpr int W = VecW<T>::v;
   const PeerView& pv = A.pv;
   const int b = blockIdx.x;
