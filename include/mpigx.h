@@ -149,6 +149,28 @@ int mpigx_allgather(const void *sendbuf, int sendcount, int sendtype, void *recv
 /* MPI_Alltoall — collective.jl:489-501 (sendbuf may be MPIGX_IN_PLACE) */
 int mpigx_alltoall(const void *sendbuf, int sendcount, int sendtype, void *recvbuf,
                    int recvcount, int recvtype, mpigx_comm_t comm);
+/* v-collectives and rooted variants.  counts/displs are
+ * host int arrays in elements, as MPI.jl passes them (Ptr{Cint}).
+ * MPI_Gather   — collective.jl:230-246 (sendbuf IN_PLACE at root) */
+int mpigx_gather(const void *sendbuf, int sendcount, int sendtype, void *recvbuf, int recvcount,
+                 int recvtype, int root, mpigx_comm_t comm);
+/* MPI_Gatherv  — collective.jl:363-382 (recvcounts/displs read at root) */
+int mpigx_gatherv(const void *sendbuf, int sendcount, int sendtype, void *recvbuf,
+                  const int *recvcounts, const int *displs, int recvtype, int root,
+                  mpigx_comm_t comm);
+/* MPI_Scatter  — collective.jl:90-106 (recvbuf IN_PLACE at root) */
+int mpigx_scatter(const void *sendbuf, int sendcount, int sendtype, void *recvbuf, int recvcount,
+                  int recvtype, int root, mpigx_comm_t comm);
+/* MPI_Scatterv — collective.jl:156-175 (sendcounts/displs read at root) */
+int mpigx_scatterv(const void *sendbuf, const int *sendcounts, const int *displs, int sendtype,
+                   void *recvbuf, int recvcount, int recvtype, int root, mpigx_comm_t comm);
+/* MPI_Allgatherv — collective.jl:424-437 (sendbuf may be MPIGX_IN_PLACE) */
+int mpigx_allgatherv(const void *sendbuf, int sendcount, int sendtype, void *recvbuf,
+                     const int *recvcounts, const int *displs, int recvtype, mpigx_comm_t comm);
+/* MPI_Alltoallv — collective.jl:545-559 (sendbuf may be MPIGX_IN_PLACE) */
+int mpigx_alltoallv(const void *sendbuf, const int *sendcounts, const int *sdispls, int sendtype,
+                    void *recvbuf, const int *recvcounts, const int *rdispls, int recvtype,
+                    mpigx_comm_t comm);
 /* MPI_Reduce   — collective.jl:605-618 (IN_PLACE at root; recvbuf ignored
  * (may be NULL) elsewhere) */
 int mpigx_reduce(const void *sendbuf, void *recvbuf, int count, int datatype, int op,

@@ -92,6 +92,29 @@ struct CopyArgs {
   void* recv;
 };
 
+// Personalised exchange (Gather(v) / Scatter(v) / Allgatherv / Alltoallv):
+// every rank stages up to n byte ranges of its send buffer into fixed slots
+// of its arena (slot j at kSlotBase + j*R), then pulls from each peer p the
+// range in p's slot p_slot[p].  Both ends of a transfer know its length, so
+// both cut it into the same G per-block slices.  One launch = one round of
+// at most R bytes of every range.
+constexpr long long kSlotBase = 256;
+struct VArgs {
+  PeerView pv;
+  long long R;          // slot size (bytes, multiple of 16)
+  long long round_off;  // byte offset of this round inside every range
+  int G;                // blocks (identical on every rank)
+  int ncopy;            // copy-in ranges: send + c_src[j] (c_len[j] bytes total) -> my slot c_slot[j]
+  int c_slot[kMaxRanks];
+  long long c_src[kMaxRanks];
+  long long c_len[kMaxRanks];
+  long long p_len[kMaxRanks];  // bytes to pull from rank p (0: nothing)
+  int p_slot[kMaxRanks];       // ... out of p's slot p_slot[p]
+  long long p_dst[kMaxRanks];  // ... into recv + p_dst[p]
+  const char* send;
+  char* recv;
+};
+
 struct ScanArgs {
   PeerView pv;
   int exclusive;

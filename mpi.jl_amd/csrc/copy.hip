@@ -104,6 +104,69 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
   rank_barrier(pv, ep++);
 }
 
+// ---------------------------------------------------------------------------
+// v-collectives (collective.jl:90-578: Scatter!/Scatterv!/Gather!/Gatherv!/
+// Allgatherv!/Alltoallv!) — SURVEY §8f next #1.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void round_slice(long long L, long long off, long long R, int G, int b, long long* lo,
+                                            long long* hi) {
+  long long len = L - off;
+  if (len < 0) len = 0;
+  if (len > R) len = R;
+  const long long sl = ((len + G - 1) / G + 15) / 16 * 16;
+  *lo = lmin((long long)b * sl, len);
+  *hi = lmin(*lo + sl, len);
+}
+
+template <int NMAX>
+__device__ __forceinline__ void vx_body(const VArgs& A) {
+  const PeerView& pv = A.pv;
+  const int b = blockIdx.x, r = pv.rank, n = pv.n;
+  uint64_t ep = pv.epoch;
+  char* mine = pv.stage[r];
+  for (int j = 0; j < A.ncopy; ++j) {
+    long long lo, hi;
+    round_slice(A.c_len[j], A.round_off, A.R, A.G, b, &lo, &hi);
+    block_copy(mine + kSlotBase + (long long)A.c_slot[j] * A.R + lo, A.send + A.c_src[j] + A.round_off + lo, hi - lo);
+  }
+  if (!rank_barrier(pv, ep++)) return;
+  char* dsts[NMAX];
+  const char* srcs[NMAX];
+  long long lens[NMAX];
+  int m = 0;
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) {
+    dsts[j] = nullptr;
+    srcs[j] = nullptr;
+    lens[j] = 0;
+    if (j < n) {
+      const int p = (r + j) % n;
+      long long lo, hi;
+      round_slice(A.p_len[p], A.round_off, A.R, A.G, b, &lo, &hi);
+      dsts[j] = A.recv + A.p_dst[p] + A.round_off + lo;
+      srcs[j] = pv.stage[p] + kSlotBase + (long long)A.p_slot[p] * A.R + lo;
+      lens[j] = hi - lo;
+      m = j + 1;
+    }
+  }
+  block_gather<NMAX>(dsts, srcs, lens, m);
+  rank_barrier(pv, ep++);
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(kThreads) void vx_kernel(VArgs A) {
+  vx_body<NMAX>(A);
+  signal_done(A.pv);
+}
+
+hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a) {
+  if (a.pv.n <= 8)
+    hipLaunchKernelGGL(vx_kernel<8>, grid, dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(vx_kernel<16>, grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a) {
   if (a.pv.n <= 8)
     hipLaunchKernelGGL(copy_kernel<8>, grid, dim3(kThreads), 0, s, a);

@@ -21,5 +21,6 @@ MPIGX_DECL_REP(bf16)
 #undef MPIGX_DECL_REP
 
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a);
+hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a);
 
 }  // namespace mpigx

@@ -174,6 +174,9 @@ struct ShmRank {
   unsigned long long sig_ptr;
   hipIpcMemHandle_t stage_h;
   hipIpcMemHandle_t sig_h;
+  // host control-plane exchange (host_allgather): double-buffered blobs
+  std::atomic<uint64_t> xseq;
+  char xbuf[2][64];
 };
 struct ShmBlock {
   std::atomic<uint64_t> magic;
@@ -221,6 +224,7 @@ struct mpigx_comm {
   unsigned long long done_target = 0;
   bool unflagged = false;  // work enqueued without the counter (stream-ordered mode)
   int sync_mode = 1;       // 1: spin on the counter, 0: hipStreamSynchronize
+  uint64_t xseq = 0;       // host_allgather sequence
   // peers (index = rank; self included)
   char* peer_stage[kMaxRanks] = {};
   uint64_t* peer_sig[kMaxRanks] = {};
@@ -404,6 +408,91 @@ int check_comm(mpigx_comm* c) {
 
 int copy_n1(mpigx_comm* c, void* dst, const void* src, size_t bytes) {
   if (dst != src && bytes) HIPCK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+  return finish(c);
+}
+
+// Host control plane: allgather of <= 64-byte blobs through the shm block
+// (double-buffered by sequence parity: a rank can only reuse a buffer after
+// every peer posted the next sequence, i.e. finished reading it).
+int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
+  if (len > 64) return MPIGX_ERR_INTERN;
+  if (c->n == 1 || !c->shm) {
+    memcpy(out, mine, len);
+    return MPIGX_SUCCESS;
+  }
+  const uint64_t k = ++c->xseq;
+  ShmRank& me = c->shm->ranks[c->rank];
+  memcpy(me.xbuf[k & 1], mine, len);
+  me.xseq.store(k, std::memory_order_release);
+  const double t0 = now_s(), limit = c->timeout_ticks / 1e8;
+  for (int q = 0; q < c->n; ++q) {
+    unsigned spins = 0;
+    while (c->shm->ranks[q].xseq.load(std::memory_order_acquire) < k) {
+      if ((++spins & 4095) == 0 && now_s() - t0 > limit) {
+        c->broken = true;
+        return MPIGX_ERR_OTHER;
+      }
+    }
+    memcpy((char*)out + (size_t)q * len, c->shm->ranks[q].xbuf[k & 1], len);
+  }
+  return MPIGX_SUCCESS;
+}
+
+// Per-rank description of a personalised exchange (see VArgs in common.hpp).
+struct VSpec {
+  int ncopy = 0;
+  int c_slot[kMaxRanks] = {};
+  long long c_src[kMaxRanks] = {};
+  long long c_len[kMaxRanks] = {};
+  long long p_len[kMaxRanks] = {};
+  int p_slot[kMaxRanks] = {};
+  long long p_dst[kMaxRanks] = {};
+  const char* send = nullptr;
+  char* recv = nullptr;
+};
+
+// Drives Gather(v)/Scatter(v)/Allgatherv/Alltoallv: agrees on the longest
+// range across ranks (host control plane), then runs ceil(max/R) rounds of
+// vx_kernel with an identical grid on every rank.
+int vexchange(mpigx_comm* c, const VSpec& s) {
+  const int n = c->n;
+  long long mx = 0;
+  for (int j = 0; j < s.ncopy; ++j) mx = s.c_len[j] > mx ? s.c_len[j] : mx;
+  for (int p = 0; p < n; ++p) mx = s.p_len[p] > mx ? s.p_len[p] : mx;
+  long long all[kMaxRanks];
+  int rc = host_allgather(c, &mx, sizeof mx, all);
+  if (rc) return rc;
+  long long gmax = 0;
+  for (int q = 0; q < n; ++q) gmax = all[q] > gmax ? all[q] : gmax;
+  if (gmax == 0) return finish(c);
+  const long long R = ((long long)(c->stage_bytes - kSlotBase) / n) & ~15ll;
+  if (R < 16) return MPIGX_ERR_NO_MEM;
+  const long long per_round = gmax < R ? gmax : R;
+  const int G = grid_for(c, per_round * n);
+  for (long long off = 0; off < gmax; off += R) {
+    VArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.R = R;
+    a.round_off = off;
+    a.G = G;
+    a.ncopy = s.ncopy;
+    for (int j = 0; j < s.ncopy; ++j) {
+      a.c_slot[j] = s.c_slot[j];
+      a.c_src[j] = s.c_src[j];
+      a.c_len[j] = s.c_len[j];
+    }
+    for (int p = 0; p < n; ++p) {
+      a.p_len[p] = s.p_len[p];
+      a.p_slot[p] = s.p_slot[p];
+      a.p_dst[p] = s.p_dst[p];
+    }
+    a.send = s.send;
+    a.recv = s.recv;
+    HIPCK(launch_vx(dim3(G), c->stream, a));
+    note_launch(c, a.pv, G);
+    c->epoch += 2;
+  }
   return finish(c);
 }
 
@@ -788,6 +877,183 @@ int mpigx_allgather(const void* sendbuf, int sendcount, int sendtype, void* recv
 int mpigx_alltoall(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
                    mpigx_comm_t c) {
   return gather_like(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, c, true);
+}
+
+// ---------------------------------------------------------------------------
+// v-collectives and rooted variants (collective.jl:90-578)
+// ---------------------------------------------------------------------------
+static int type_bytes(int dtype, long long count, long long* out) {
+  const TypeInfo* t = find_type(dtype);
+  if (!t) return MPIGX_ERR_TYPE;
+  if (count < 0) return MPIGX_ERR_COUNT;
+  *out = count * t->size;
+  return MPIGX_SUCCESS;
+}
+
+// MPI_Gather / MPI_Gatherv (collective.jl:230-246, 363-382).  counts/displs
+// (in recvtype elements) are read at the root only; NULL => equal blocks.
+static int gather_common(const void* send, int scount, int stype, void* recv, int rcount, const int* rcounts,
+                         const int* displs, int rtype, int root, mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const int n = c->n, r = c->rank;
+  if (root < 0 || root >= n) return MPIGX_ERR_ROOT;
+  const bool isroot = r == root, inplace = send == MPIGX_IN_PLACE;
+  if (inplace && !isroot) return MPIGX_ERR_BUFFER;
+  VSpec s;
+  int rsz = 0;
+  if (isroot) {
+    if ((rc = mpigx_type_size(rtype, &rsz))) return rc;
+    if (!recv) return MPIGX_ERR_BUFFER;
+    for (int p = 0; p < n; ++p) {
+      const long long cnt = rcounts ? rcounts[p] : rcount;
+      if (cnt < 0) return MPIGX_ERR_COUNT;
+      const long long dsp = rcounts ? displs[p] : (long long)p * rcount;
+      s.p_len[p] = cnt * rsz;
+      s.p_slot[p] = 0;
+      s.p_dst[p] = dsp * rsz;
+    }
+    if (inplace) s.p_len[r] = 0;
+  }
+  if (!inplace) {
+    long long sb;
+    if ((rc = type_bytes(stype, scount, &sb))) return rc;
+    if (sb && !send) return MPIGX_ERR_BUFFER;
+    s.ncopy = 1;
+    s.c_slot[0] = 0;
+    s.c_src[0] = 0;
+    s.c_len[0] = sb;
+  }
+  s.send = (const char*)send;
+  s.recv = (char*)recv;
+  return vexchange(c, s);
+}
+
+int mpigx_gather(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
+                 int root, mpigx_comm_t c) {
+  return gather_common(sendbuf, sendcount, sendtype, recvbuf, recvcount, nullptr, nullptr, recvtype, root, c);
+}
+int mpigx_gatherv(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, const int* recvcounts,
+                  const int* displs, int recvtype, int root, mpigx_comm_t c) {
+  if (c && c->rank == root && (!recvcounts || !displs)) return MPIGX_ERR_ARG;
+  return gather_common(sendbuf, sendcount, sendtype, recvbuf, 0, recvcounts, displs, recvtype, root, c);
+}
+
+// MPI_Scatter / MPI_Scatterv (collective.jl:90-106, 156-175).
+static int scatter_common(const void* send, int scount, const int* scounts, const int* displs, int stype, void* recv,
+                          int rcount, int rtype, int root, mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const int n = c->n, r = c->rank;
+  if (root < 0 || root >= n) return MPIGX_ERR_ROOT;
+  const bool isroot = r == root, inplace = recv == MPIGX_IN_PLACE;
+  if (inplace && !isroot) return MPIGX_ERR_BUFFER;
+  VSpec s;
+  if (isroot) {
+    int ssz = 0;
+    if ((rc = mpigx_type_size(stype, &ssz))) return rc;
+    if (!send) return MPIGX_ERR_BUFFER;
+    s.ncopy = n;
+    for (int q = 0; q < n; ++q) {
+      const long long cnt = scounts ? scounts[q] : scount;
+      if (cnt < 0) return MPIGX_ERR_COUNT;
+      const long long dsp = scounts ? displs[q] : (long long)q * scount;
+      s.c_slot[q] = q;
+      s.c_src[q] = dsp * ssz;
+      s.c_len[q] = (inplace && q == r) ? 0 : cnt * ssz;
+    }
+  }
+  if (!inplace) {
+    long long rb;
+    if ((rc = type_bytes(rtype, rcount, &rb))) return rc;
+    if (rb && !recv) return MPIGX_ERR_BUFFER;
+    s.p_len[root] = rb;
+    s.p_slot[root] = r;
+    s.p_dst[root] = 0;
+  }
+  s.send = (const char*)send;
+  s.recv = (char*)recv;
+  return vexchange(c, s);
+}
+
+int mpigx_scatter(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
+                  int root, mpigx_comm_t c) {
+  return scatter_common(sendbuf, sendcount, nullptr, nullptr, sendtype, recvbuf, recvcount, recvtype, root, c);
+}
+int mpigx_scatterv(const void* sendbuf, const int* sendcounts, const int* displs, int sendtype, void* recvbuf,
+                   int recvcount, int recvtype, int root, mpigx_comm_t c) {
+  if (c && c->rank == root && (!sendcounts || !displs)) return MPIGX_ERR_ARG;
+  return scatter_common(sendbuf, 0, sendcounts, displs, sendtype, recvbuf, recvcount, recvtype, root, c);
+}
+
+// MPI_Allgatherv (collective.jl:424-437)
+int mpigx_allgatherv(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, const int* recvcounts,
+                     const int* displs, int recvtype, mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  if (!recvcounts || !displs) return MPIGX_ERR_ARG;
+  const int n = c->n, r = c->rank;
+  int rsz = 0;
+  if ((rc = mpigx_type_size(recvtype, &rsz))) return rc;
+  const bool inplace = sendbuf == MPIGX_IN_PLACE;
+  VSpec s;
+  for (int p = 0; p < n; ++p) {
+    if (recvcounts[p] < 0) return MPIGX_ERR_COUNT;
+    s.p_len[p] = (long long)recvcounts[p] * rsz;
+    s.p_slot[p] = 0;
+    s.p_dst[p] = (long long)displs[p] * rsz;
+  }
+  if (!recvbuf && s.p_len[r]) return MPIGX_ERR_BUFFER;
+  s.ncopy = 1;
+  s.c_slot[0] = 0;
+  if (inplace) {
+    s.send = (const char*)recvbuf;
+    s.c_src[0] = s.p_dst[r];
+    s.c_len[0] = s.p_len[r];
+    s.p_len[r] = 0;
+  } else {
+    long long sb;
+    if ((rc = type_bytes(sendtype, sendcount, &sb))) return rc;
+    if (sb && !sendbuf) return MPIGX_ERR_BUFFER;
+    s.send = (const char*)sendbuf;
+    s.c_src[0] = 0;
+    s.c_len[0] = sb;
+  }
+  s.recv = (char*)recvbuf;
+  return vexchange(c, s);
+}
+
+// MPI_Alltoallv (collective.jl:545-559); MPI-2.2 IN_PLACE takes the send
+// layout from recvcounts/rdispls.
+int mpigx_alltoallv(const void* sendbuf, const int* sendcounts, const int* sdispls, int sendtype, void* recvbuf,
+                    const int* recvcounts, const int* rdispls, int recvtype, mpigx_comm_t c) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  if (!recvcounts || !rdispls) return MPIGX_ERR_ARG;
+  const int n = c->n, r = c->rank;
+  const bool inplace = sendbuf == MPIGX_IN_PLACE;
+  int rsz = 0, ssz = 0;
+  if ((rc = mpigx_type_size(recvtype, &rsz))) return rc;
+  if (!inplace) {
+    if (!sendcounts || !sdispls) return MPIGX_ERR_ARG;
+    if ((rc = mpigx_type_size(sendtype, &ssz))) return rc;
+  }
+  VSpec s;
+  s.ncopy = n;
+  for (int q = 0; q < n; ++q) {
+    const long long sc = inplace ? recvcounts[q] : sendcounts[q];
+    const long long sd = inplace ? rdispls[q] : sdispls[q];
+    if (sc < 0 || recvcounts[q] < 0) return MPIGX_ERR_COUNT;
+    s.c_slot[q] = q;
+    s.c_src[q] = sd * (inplace ? rsz : ssz);
+    s.c_len[q] = sc * (inplace ? rsz : ssz);
+    s.p_len[q] = (long long)recvcounts[q] * rsz;
+    s.p_slot[q] = r;
+    s.p_dst[q] = (long long)rdispls[q] * rsz;
+  }
+  s.send = inplace ? (const char*)recvbuf : (const char*)sendbuf;
+  s.recv = (char*)recvbuf;
+  return vexchange(c, s);
 }
 
 int mpigx_allreduce(const void* sendbuf, void* recvbuf, int count, int datatype, int op, mpigx_comm_t c) {

@@ -18,6 +18,9 @@ _lib = None
 c_int, c_void_p, c_longlong, c_size_t = ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_size_t
 
 
+_IP = ctypes.POINTER(ctypes.c_int)
+
+
 class UniqueId(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]
 
@@ -43,6 +46,12 @@ PROTOTYPES = {
     "mpigx_bcast": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "mpigx_allgather": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
     "mpigx_alltoall": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "mpigx_gather": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mpigx_gatherv": (c_int, [c_void_p, c_int, c_int, c_void_p, _IP, _IP, c_int, c_int, c_void_p]),
+    "mpigx_scatter": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mpigx_scatterv": (c_int, [c_void_p, _IP, _IP, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mpigx_allgatherv": (c_int, [c_void_p, c_int, c_int, c_void_p, _IP, _IP, c_int, c_void_p]),
+    "mpigx_alltoallv": (c_int, [c_void_p, _IP, _IP, c_int, c_void_p, _IP, _IP, c_int, c_void_p]),
     "mpigx_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "mpigx_allreduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mpigx_scan": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),

@@ -573,6 +573,167 @@ def Alltoall(sendbuf, count, comm):
     return Alltoall_(sendbuf, _empty_like(sendbuf, Comm_size(comm) * count), count, comm)
 
 
+# ---------------------------------------------------------------------------
+# v-collectives and rooted variants (collective.jl:90-578)
+# ---------------------------------------------------------------------------
+def _cints(xs):
+    xs = [int(x) for x in xs]
+    return (ctypes.c_int * max(1, len(xs)))(*xs)
+
+
+def _disps(counts):
+    """accumulate(+, counts) - counts (collective.jl:169, :365, :425, :551)."""
+    d, acc = [], 0
+    for c in counts:
+        d.append(acc)
+        acc += int(c)
+    return d
+
+
+def Scatter_(sendbuf, recvbuf, *args):
+    """Scatter!(sendbuf, recvbuf[, count], root, comm) — collective.jl:90-112.
+    `recvbuf = None` at the root means MPI_IN_PLACE."""
+    if len(args) == 2:
+        root, comm = args
+        count = _len(recvbuf)
+    else:
+        count, root, comm = args
+    isroot = Comm_rank(comm) == root
+    if isroot:
+        assert sendbuf is not None
+        _assert_minlength(sendbuf, count * Comm_size(comm))
+        if recvbuf is None:
+            recvbuf = IN_PLACE
+    _assert_minlength(recvbuf, count)
+    T = _eltype(sendbuf) if recvbuf is IN_PLACE else _eltype(recvbuf)
+    data = sendbuf if recvbuf is IN_PLACE or recvbuf is None else recvbuf
+    _call("Scatter", data, comm, _ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val, int(root))
+    return recvbuf
+
+
+def Scatter(sendbuf, count, root, comm):
+    """collective.jl:127-129."""
+    return Scatter_(sendbuf, _empty_like(sendbuf, count), count, root, comm)
+
+
+def Scatterv_(sendbuf, recvbuf, counts, root, comm):
+    """Scatterv!(sendbuf, recvbuf, counts, root, comm) — collective.jl:156-175."""
+    rank = Comm_rank(comm)
+    if rank == root:
+        assert sendbuf is not None
+        _assert_minlength(sendbuf, sum(counts))
+    if recvbuf is None:
+        recvbuf = IN_PLACE
+    _assert_minlength(recvbuf, counts[rank])
+    T = _eltype(sendbuf) if recvbuf is IN_PLACE else _eltype(recvbuf)
+    data = sendbuf if recvbuf is IN_PLACE else recvbuf
+    _call("Scatterv", data, comm, _ptr(sendbuf), _cints(counts), _cints(_disps(counts)), T.val, _ptr(recvbuf),
+          int(counts[rank]), T.val, int(root))
+    return recvbuf
+
+
+def Scatterv(sendbuf, counts, root, comm):
+    """collective.jl:193-196."""
+    return Scatterv_(sendbuf, _empty_like(sendbuf, counts[Comm_rank(comm)]), counts, root, comm)
+
+
+def Gather_(sendbuf, recvbuf, *args):
+    """Gather!(sendbuf, recvbuf[, count=length(sendbuf)], root, comm) — collective.jl:230-251.
+    `sendbuf = None` at the root means MPI_IN_PLACE; returns recvbuf at root, None elsewhere."""
+    if len(args) == 2:
+        root, comm = args
+        count = _len(sendbuf)
+    else:
+        count, root, comm = args
+    isroot = Comm_rank(comm) == root
+    if isroot:
+        assert recvbuf is not None
+        _assert_minlength(recvbuf, count * Comm_size(comm))
+        if sendbuf is None:
+            sendbuf = IN_PLACE
+    _assert_minlength(sendbuf, count)
+    T = _eltype(recvbuf) if sendbuf is IN_PLACE else _eltype(sendbuf)
+    data = recvbuf if sendbuf is IN_PLACE else sendbuf
+    _call("Gather", data, comm, _ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val, int(root))
+    return recvbuf if isroot else None
+
+
+def Gather(*args):
+    """Gather(sendbuf[, count], root, comm) / Gather(obj, root, comm) — collective.jl:267-275."""
+    if len(args) == 4:
+        sendbuf, count, root, comm = args
+        recv = _empty_like(sendbuf, Comm_size(comm) * count) if Comm_rank(comm) == root else None
+        return Gather_(sendbuf, recv, count, root, comm)
+    sendbuf, root, comm = args
+    if _is_array(sendbuf):
+        return Gather(sendbuf, _len(sendbuf), root, comm)
+    ref = _scalar_ref(sendbuf, comm)
+    recv = _empty_like(ref, Comm_size(comm)) if Comm_rank(comm) == root else None
+    out = Gather_(ref, recv, 1, root, comm)
+    return None if out is None else (out if isinstance(out, np.ndarray) else out.cpu().numpy()).tolist()
+
+
+def Gatherv_(sendbuf, recvbuf, counts, root, comm):
+    """Gatherv!(sendbuf, recvbuf, counts, root, comm) — collective.jl:363-382."""
+    rank = Comm_rank(comm)
+    isroot = rank == root
+    if isroot:
+        assert recvbuf is not None
+        _assert_minlength(recvbuf, sum(counts))
+        if sendbuf is None:
+            sendbuf = IN_PLACE
+    _assert_minlength(sendbuf, counts[rank])
+    T = _eltype(recvbuf) if sendbuf is IN_PLACE else _eltype(sendbuf)
+    data = recvbuf if sendbuf is IN_PLACE else sendbuf
+    _call("Gatherv", data, comm, _ptr(sendbuf), int(counts[rank]), T.val, _ptr(recvbuf), _cints(counts),
+          _cints(_disps(counts)), T.val, int(root))
+    return recvbuf if isroot else None
+
+
+def Gatherv(sendbuf, counts, root, comm):
+    """collective.jl:401-403."""
+    recv = _empty_like(sendbuf, sum(counts)) if Comm_rank(comm) == root else None
+    return Gatherv_(sendbuf, recv, counts, root, comm)
+
+
+def Allgatherv_(*args):
+    """Allgatherv!(sendbuf, recvbuf, counts, comm) / Allgatherv!(sendrecvbuf, counts, comm)
+    — collective.jl:424-442."""
+    if len(args) == 3:
+        sendbuf, (recvbuf, counts, comm) = IN_PLACE, args
+    else:
+        sendbuf, recvbuf, counts, comm = args
+    sendcnt = counts[Comm_rank(comm)]
+    assert recvbuf is not None
+    _assert_minlength(recvbuf, sum(counts))
+    _assert_minlength(sendbuf, sendcnt)
+    T = _eltype(recvbuf)
+    _call("Allgatherv", recvbuf, comm, _ptr(sendbuf), int(sendcnt), T.val, _ptr(recvbuf), _cints(counts),
+          _cints(_disps(counts)), T.val)
+    return recvbuf
+
+
+def Allgatherv(sendbuf, counts, comm):
+    """collective.jl:458-461."""
+    return Allgatherv_(sendbuf, _empty_like(sendbuf, sum(counts)), counts, comm)
+
+
+def Alltoallv_(sendbuf, recvbuf, scounts, rcounts, comm):
+    """Alltoallv!(sendbuf, recvbuf, scounts, rcounts, comm) — collective.jl:545-559."""
+    _assert_minlength(sendbuf, sum(scounts))
+    _assert_minlength(recvbuf, sum(rcounts))
+    assert _eltype(sendbuf) == _eltype(recvbuf)
+    T = _eltype(sendbuf)
+    _call("Alltoallv", recvbuf, comm, _ptr(sendbuf), _cints(scounts), _cints(_disps(scounts)), T.val,
+          _ptr(recvbuf), _cints(rcounts), _cints(_disps(rcounts)), T.val)
+    return recvbuf
+
+
+def Alltoallv(sendbuf, scounts, rcounts, comm):
+    """collective.jl:574-578."""
+    return Alltoallv_(sendbuf, _empty_like(sendbuf, sum(rcounts)), scounts, rcounts, comm)
+
+
 def _scalar_ref(obj, comm):
     """`Ref(object)` of the scalar forms: a 1-element host array when host
     libmpi is up (as in MPI.jl), else a 1-element device tensor."""

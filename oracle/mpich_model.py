@@ -408,3 +408,53 @@ def fold_tree(inputs, dtname, opname):
 def fold_rsag(inputs, dtname, opname):
     """MPICH single-node Allreduce result in the Rabenseifner regime."""
     return _allreduce_rsag(list(inputs), dtname, opname)[0]
+
+
+# ---------------------------------------------------------------------------
+# v-collectives / rooted variants (byte movement; MPI.jl passes packed
+# displacements: disps = cumsum(counts) - counts, collective.jl:169/365/425/551)
+# ---------------------------------------------------------------------------
+def vcnt(seed, a, b, base):
+    """Count pattern of the golden v-cases (gen_mpich_golden.c vcnt)."""
+    return ((a * 7 + b * 3 + seed) % 5) * base
+
+
+def _disps(counts):
+    d, acc = [], 0
+    for c in counts:
+        d.append(acc)
+        acc += c
+    return d
+
+
+def gather(inputs, count, root):
+    """Result at root of MPI_Gather (collective.jl:230-246)."""
+    return np.concatenate([x[:count] for x in inputs])
+
+
+def gatherv(inputs, counts):
+    """Result at root of MPI_Gatherv (collective.jl:363-382)."""
+    return np.concatenate([x[:c] for x, c in zip(inputs, counts)])
+
+
+def scatter(root_buf, count, n):
+    """Per-rank outputs of MPI_Scatter (collective.jl:90-106)."""
+    return [root_buf[r * count:(r + 1) * count].copy() for r in range(n)]
+
+
+def scatterv(root_buf, counts):
+    """Per-rank outputs of MPI_Scatterv (collective.jl:156-175)."""
+    d = _disps(counts)
+    return [root_buf[d[r]:d[r] + counts[r]].copy() for r in range(len(counts))]
+
+
+def allgatherv(inputs, counts):
+    full = gatherv(inputs, counts)
+    return [full.copy() for _ in inputs]
+
+
+def alltoallv(inputs, S):
+    """S[p][q] = elements rank p sends to rank q (collective.jl:545-559)."""
+    n = len(inputs)
+    sd = [_disps(S[p]) for p in range(n)]
+    return [np.concatenate([inputs[p][sd[p][r]:sd[p][r] + S[p][r]] for p in range(n)]) for r in range(n)]

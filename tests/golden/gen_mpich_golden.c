@@ -190,6 +190,72 @@ static void run_case(const char *coll, const char *dtn, const char *opn, int cou
     free(out);
 }
 
+/* v-collectives: counts are a deterministic function of (seed, a, b) and may
+ * be 0; displacements are packed (MPI.jl: disps = cumsum(counts) - counts,
+ * collective.jl:169, :365, :425, :551-552).  Buffers are padded to the
+ * largest rank's size so the dumps stay rectangular. */
+static int vcnt(int seed, int a, int b, int base) { return ((a * 7 + b * 3 + seed) % 5) * base; }
+
+static void run_vcase(const char *coll, const char *dtn, int base, int root, int seed) {
+    const DT *d = dt_by_name(dtn);
+    int n = g_size, r = g_rank;
+    char id[256];
+    snprintf(id, sizeof id, "n%d_%04d", n, case_no++);
+    int cnt[16][16], sc[16], sd[16], rc_[16], rd[16];
+    for (int a = 0; a < 16; a++)
+        for (int b = 0; b < 16; b++) cnt[a][b] = vcnt(seed, a, b, base);
+    size_t in_max = 0, out_max = 0, myin = 0, myout = 0;
+    for (int q = 0; q < n; q++) {
+        size_t i = 0, o = 0;
+        if (!strcmp(coll, "gather")) { i = base; o = q == root ? (size_t)n * base : 0; }
+        if (!strcmp(coll, "gatherv")) { i = cnt[q][0]; if (q == root) for (int p = 0; p < n; p++) o += cnt[p][0]; }
+        if (!strcmp(coll, "scatter")) { i = q == root ? (size_t)n * base : 0; o = base; }
+        if (!strcmp(coll, "scatterv")) { if (q == root) for (int p = 0; p < n; p++) i += cnt[p][1]; o = cnt[q][1]; }
+        if (!strcmp(coll, "allgatherv")) { i = cnt[q][2]; for (int p = 0; p < n; p++) o += cnt[p][2]; }
+        if (!strcmp(coll, "alltoallv")) { for (int p = 0; p < n; p++) { i += cnt[q][p]; o += cnt[p][q]; } }
+        if (i > in_max) in_max = i;
+        if (o > out_max) out_max = o;
+        if (q == r) { myin = i; myout = o; }
+    }
+    size_t ib = in_max * d->esize + 16, ob = out_max * d->esize + 16;
+    unsigned char *in = calloc(ib, 1), *out = malloc(ob);
+    gen(in, d, (int)myin, r, n, seed, G_RAND);
+    memset(out, 0xCD, ob);
+    int rc = 0, acc = 0;
+    if (!strcmp(coll, "gather")) rc = MPI_Gather(in, base, d->dt, out, base, d->dt, root, MPI_COMM_WORLD);
+    else if (!strcmp(coll, "scatter")) rc = MPI_Scatter(in, base, d->dt, out, base, d->dt, root, MPI_COMM_WORLD);
+    else if (!strcmp(coll, "gatherv")) {
+        for (int p = 0; p < n; p++) { rc_[p] = cnt[p][0]; rd[p] = acc; acc += rc_[p]; }
+        rc = MPI_Gatherv(in, cnt[r][0], d->dt, out, rc_, rd, d->dt, root, MPI_COMM_WORLD);
+    } else if (!strcmp(coll, "scatterv")) {
+        for (int p = 0; p < n; p++) { sc[p] = cnt[p][1]; sd[p] = acc; acc += sc[p]; }
+        rc = MPI_Scatterv(in, sc, sd, d->dt, out, cnt[r][1], d->dt, root, MPI_COMM_WORLD);
+    } else if (!strcmp(coll, "allgatherv")) {
+        for (int p = 0; p < n; p++) { rc_[p] = cnt[p][2]; rd[p] = acc; acc += rc_[p]; }
+        rc = MPI_Allgatherv(in, cnt[r][2], d->dt, out, rc_, rd, d->dt, MPI_COMM_WORLD);
+    } else if (!strcmp(coll, "alltoallv")) {
+        int a2 = 0;
+        for (int p = 0; p < n; p++) { sc[p] = cnt[r][p]; sd[p] = acc; acc += sc[p]; rc_[p] = cnt[p][r]; rd[p] = a2; a2 += rc_[p]; }
+        rc = MPI_Alltoallv(in, sc, sd, d->dt, out, rc_, rd, d->dt, MPI_COMM_WORLD);
+    } else abort();
+    dump(id, "in", in, ib);
+    dump(id, "out", out, ob);
+    if (g_rank == 0) {
+        fprintf(manifest, "{\"id\":\"%s\",\"coll\":\"%s\",\"n\":%d,\"dtype\":\"%s\",\"op\":null,\"count\":%d,\"root\":%d,"
+                "\"mode\":0,\"seed\":%d,\"rc\":%d,\"in_bytes\":%zu,\"out_bytes\":%zu,\"counts\":[",
+                id, coll, n, dtn, base, root, seed, rc, ib, ob);
+        for (int a = 0; a < n; a++) {
+            fprintf(manifest, "%s[", a ? "," : "");
+            for (int b = 0; b < n; b++) fprintf(manifest, "%s%d", b ? "," : "", cnt[a][b]);
+            fprintf(manifest, "]");
+        }
+        fprintf(manifest, "]}\n");
+        fflush(manifest);
+    }
+    free(in);
+    free(out);
+}
+
 /* single-process probe of the op x type matrix and of the elementwise
  * semantics of MPI_Reduce_local(inbuf, inoutbuf) (mpi.h:1357) */
 static void reduce_local_probe(void) {
@@ -313,6 +379,13 @@ int main(int argc, char **argv) {
         run_case("allgather", "C_DOUBLE_COMPLEX", NULL, 37, 0, G_RAND, 504);
         run_case("alltoall", "FLOAT", NULL, 1, 0, G_RANKP1, 505);
         run_case("alltoall", "INT16_T", NULL, 129, 0, G_RAND, 506);
+        /* --- v-collectives / rooted variants --- */
+        const char *vcolls[] = {"gather", "gatherv", "scatter", "scatterv", "allgatherv", "alltoallv"};
+        for (int v = 0; v < 6; v++) {
+            run_vcase(vcolls[v], "FLOAT", 1, 0, 601 + v);
+            run_vcase(vcolls[v], "INT8_T", 37, n - 1, 611 + v);
+            run_vcase(vcolls[v], "C_DOUBLE_COMPLEX", 29, n / 2, 621 + v);
+        }
     }
     if (g_rank == 0) fclose(manifest);
     MPI_Finalize();

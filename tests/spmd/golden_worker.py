@@ -110,7 +110,8 @@ class Runner:
     def golden(self):
         cases, arr = load()
         for c in cases:
-            if c["n"] != self.n or c["coll"] == "reduce_local":
+            if c["n"] != self.n or c["coll"] in ("reduce_local", "gather", "gatherv", "scatter", "scatterv",
+                                                 "allgatherv", "alltoallv"):
                 continue
             npdt = M.DTYPES[c["dtype"]][1]
             ins = typed(arr[c["id"] + ".in"], npdt)
@@ -132,6 +133,94 @@ class Runner:
                         continue
                     self.check(same_bits(got, exp), (c["id"], coll, c["dtype"], c["op"], algo, inplace))
         os.environ.pop("MPIGX_ALGO", None)
+
+    def vgolden(self):
+        """Gather(v)/Scatter(v)/Allgatherv/Alltoallv golden cases (MPICH) through the C ABI,
+        regular and IN_PLACE forms; the bytes past the result must stay untouched."""
+        from test_oracle_golden import v_expected
+        cases, arr = load()
+        L, r, n, cv = self.L, self.r, self.n, self.comm.val
+        I = ctypes.c_int * 16
+        for c in cases:
+            if c["n"] != n or "counts" not in c:
+                continue
+            npdt = M.DTYPES[c["dtype"]][1]
+            h = M.DTYPES[c["dtype"]][0]
+            es = np.dtype(npdt).itemsize
+            ins = typed(arr[c["id"] + ".in"], npdt)
+            seed, base, root, coll = c["seed"], c["count"], c["root"], c["coll"]
+            K = [[M.vcnt(seed, a, b, base) for b in range(16)] for a in range(16)]
+            exp = v_expected(c, ins).get(r)
+            for inplace in (False, True):
+                outn = (exp.size if exp is not None else 0) + 8
+                recv = dev(np.full(outn * es, 0xCD, np.uint8))
+                x = ins[r]
+                if coll == "gather":
+                    if inplace and r == root:
+                        full = np.full(outn * es, 0xCD, np.uint8)
+                        full[r * base * es:(r + 1) * base * es] = x[:base].view(np.uint8)
+                        recv = dev(full)
+                        rc = L.mpigx_gather(IN_PLACE, 0, 0, P(recv), base, h, root, cv)
+                    else:
+                        rc = L.mpigx_gather(P(dev(x[:base])), base, h, P(recv), base, h, root, cv)
+                elif coll == "gatherv":
+                    cnts = [K[p][0] for p in range(n)]
+                    ds = [sum(cnts[:p]) for p in range(n)]
+                    if inplace and r == root:
+                        full = np.full(outn * es, 0xCD, np.uint8)
+                        full[ds[r] * es:(ds[r] + cnts[r]) * es] = x[:cnts[r]].view(np.uint8)
+                        recv = dev(full)
+                        rc = L.mpigx_gatherv(IN_PLACE, 0, 0, P(recv), I(*cnts), I(*ds), h, root, cv)
+                    else:
+                        rc = L.mpigx_gatherv(P(dev(x[:cnts[r]])), cnts[r], h, P(recv), I(*cnts), I(*ds), h, root, cv)
+                elif coll in ("scatter", "scatterv"):
+                    cnts = [base] * n if coll == "scatter" else [K[p][1] for p in range(n)]
+                    ds = [sum(cnts[:p]) for p in range(n)]
+                    sb = P(dev(x)) if r == root else None
+                    if inplace and r == root:
+                        rc = (L.mpigx_scatter(sb, base, h, IN_PLACE, 0, 0, root, cv) if coll == "scatter" else
+                              L.mpigx_scatterv(sb, I(*cnts), I(*ds), h, IN_PLACE, 0, 0, root, cv))
+                        exp_r = None
+                    else:
+                        rc = (L.mpigx_scatter(sb, base, h, P(recv), base, h, root, cv) if coll == "scatter" else
+                              L.mpigx_scatterv(sb, I(*cnts), I(*ds), h, P(recv), cnts[r], h, root, cv))
+                elif coll == "allgatherv":
+                    cnts = [K[p][2] for p in range(n)]
+                    ds = [sum(cnts[:p]) for p in range(n)]
+                    if inplace:
+                        full = np.full(outn * es, 0xCD, np.uint8)
+                        full[ds[r] * es:(ds[r] + cnts[r]) * es] = x[:cnts[r]].view(np.uint8)
+                        recv = dev(full)
+                        rc = L.mpigx_allgatherv(IN_PLACE, 0, 0, P(recv), I(*cnts), I(*ds), h, cv)
+                    else:
+                        rc = L.mpigx_allgatherv(P(dev(x[:cnts[r]])), cnts[r], h, P(recv), I(*cnts), I(*ds), h, cv)
+                else:  # alltoallv
+                    S = [[K[p][q] for q in range(n)] for p in range(n)]
+                    sc = S[r]
+                    sd = [sum(sc[:q]) for q in range(n)]
+                    rcn = [S[p][r] for p in range(n)]
+                    rd = [sum(rcn[:p]) for p in range(n)]
+                    if inplace:
+                        continue  # in-place alltoallv needs send layout == recv layout; covered below
+                    rc = L.mpigx_alltoallv(P(dev(x[:sum(sc)])), I(*sc), I(*sd), h, P(recv), I(*rcn), I(*rd), h, cv)
+                self.check(rc == 0, (c["id"], coll, "rc", rc))
+                if exp is None or (coll in ("scatter", "scatterv") and inplace and r == root):
+                    continue
+                got = host(recv, np.uint8)
+                ok = np.array_equal(got[:exp.nbytes], exp.view(np.uint8)) and (got[exp.nbytes:] == 0xCD).all()
+                self.check(ok, (c["id"], coll, r, "inplace" if inplace else ""))
+        # in-place alltoallv with a symmetric layout (recvcounts define the send layout too)
+        cnt = [(p * 3 + r) % 4 + 1 for p in range(n)]  # rank r sends cnt[q] to q; symmetric needs S[p][r] == S[r][p]
+        S = [[(p * 3 + q) % 4 + 1 + (q * 3 + p) % 4 for q in range(n)] for p in range(n)]
+        sym = [[S[p][q] + S[q][p] for q in range(n)] for p in range(n)]
+        ins = [np.arange(sum(sym[p]), dtype=np.float32) + 1000 * p for p in range(n)]
+        rcn = [sym[p][r] for p in range(n)]
+        rd = [sum(rcn[:p]) for p in range(n)]
+        buf = dev(ins[r])
+        rc = L.mpigx_alltoallv(IN_PLACE, None, None, 0, P(buf), I(*rcn), I(*rd), M.DTYPES["FLOAT"][0], cv)
+        self.check(rc == 0, "alltoallv inplace rc")
+        self.check(same_bits(host(buf, np.float32), M.alltoallv(ins, sym)[r]), "alltoallv inplace")
+        del cnt
 
     def oracle_cases(self, sizes):
         """Larger seeded cases vs the (MPICH-pinned) oracle."""
@@ -191,6 +280,7 @@ def main():
     R = Runner(comm)
     phase = os.environ.get("MPIGX_TEST_PHASE", "all")
     R.golden()
+    R.vgolden()
     R.errors()
     R.oracle_cases([("FLOAT", "SUM", 1_000_003), ("DOUBLE", "SUM", 65537), ("FLOAT", "MAX", 100_001),
                     ("INT32_T", "BAND", 262_147), ("INT64_T", "MAX", 50_000), ("BFLOAT16", "SUM", 40_000),

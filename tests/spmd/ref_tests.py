@@ -289,9 +289,149 @@ def t_alltoall(comm):
         check(eq(a, np.arange(size, dtype=T)), ("alltoall IN_PLACE", T.__name__))
 
 
+def t_gather(comm):
+    """test/test_gather.jl:12-70"""
+    root, rank, sz = 0, MPI.Comm_rank(comm), MPI.Comm_size(comm)
+    isroot = rank == root
+    for T in TYPES:
+        A = arr(np.full(4, rank + 1), T)
+        C = MPI.Gather(A, root, comm)
+        if isroot:
+            check(is_array_type(C, T), "gather type")
+            check(eq(C, np.repeat(np.arange(1, sz + 1), 4).astype(T)), ("gather", T.__name__))
+        Cs = MPI.Gather(T(rank + 1), root, comm)
+        if isroot:
+            check(isinstance(Cs, list) and Cs == list(np.arange(1, sz + 1, dtype=T)), ("gather obj", T.__name__))
+        A = arr([rank + 1, 0], T)
+        C = MPI.Gather(A, 1, root, comm)
+        if isroot:
+            check(eq(C, np.arange(1, sz + 1, dtype=T)), "gather explicit length")
+        C = MPI.Gather(A[0:1], root, comm)  # view(A, 1:1)
+        if isroot:
+            check(eq(C, np.arange(1, sz + 1, dtype=T)), "gather view")
+        A = arr(np.full(4, rank + 1), T)
+        C = undef(4 * sz, T)
+        MPI.Gather_(A, C, _len(A), root, comm)
+        if isroot:
+            check(eq(C, np.repeat(np.arange(1, sz + 1), 4).astype(T)), "gather!")
+        A = arr(np.full(4 * sz if isroot else 4, rank + 1), T)
+        if isroot:
+            MPI.Gather_(None, A, 4, root, comm)
+            check(eq(A, np.repeat(np.arange(1, sz + 1), 4).astype(T)), ("gather IN_PLACE", T.__name__))
+        else:
+            MPI.Gather_(A, None, 4, root, comm)
+
+
+def t_gatherv(comm):
+    """test/test_gatherv.jl:12-58"""
+    root, size, rank = 0, MPI.Comm_size(comm), MPI.Comm_rank(comm)
+    isroot = rank == root
+    counts = [i % 2 + 1 for i in range(size)]
+    chk = np.concatenate([np.full(counts[r], r) for r in range(size)])
+    for T in TYPES:
+        A = arr(np.full(rank % 2 + 1, rank), T)
+        B = MPI.Gatherv(A, counts, root, comm)
+        if isroot:
+            check(is_array_type(B, T) and eq(B, chk.astype(T)), ("gatherv", T.__name__))
+        B = undef(sum(counts), T)
+        MPI.Gatherv_(A, B, counts, root, comm)
+        if isroot:
+            check(eq(B, chk.astype(T)), "gatherv!")
+        B = undef(sum(counts) - 1, T)
+        if isroot:
+            raises(AssertionError, lambda: MPI.Gatherv_(A, B, counts, root, comm), "gatherv short")
+        B = arr(np.full(sum(counts), rank), T)
+        if isroot:
+            MPI.Gatherv_(None, B, counts, root, comm)
+            check(eq(B, chk.astype(T)), ("gatherv IN_PLACE", T.__name__))
+        else:
+            MPI.Gatherv_(B, None, counts, root, comm)
+
+
+def t_scatter(comm):
+    """test/test_scatter.jl:12-44"""
+    size, rank, root = MPI.Comm_size(comm), MPI.Comm_rank(comm), 0
+    isroot = rank == root
+    for T in TYPES:
+        A = arr(np.arange(1, size + 1), T) if isroot else undef(1, T)
+        B = MPI.Scatter(A, 1, root, comm)
+        check(is_array_type(B, T) and host(B)[0] == T(rank + 1), ("scatter", T.__name__))
+        B = undef(1, T)
+        MPI.Scatter_(A, B, 1, root, comm)
+        check(host(B)[0] == T(rank + 1), "scatter!")
+        B = copy(A) if isroot else undef(1, T)
+        if isroot:
+            MPI.Scatter_(B, None, 1, root, comm)
+        else:
+            MPI.Scatter_(None, B, 1, root, comm)
+        check(host(B)[0] == T(rank + 1), ("scatter IN_PLACE", T.__name__))
+        B = undef(0, T)
+        raises(AssertionError, lambda: MPI.Scatter_(A, B, 1, root, comm), "scatter short")
+
+
+def t_scatterv(comm):
+    """test/test_scatterv.jl:12-50"""
+    size, rank, root = MPI.Comm_size(comm), MPI.Comm_rank(comm), 0
+    isroot = rank == root
+    counts = [i % 2 + 1 for i in range(size)]
+    ref = np.concatenate([np.full(counts[r], r) for r in range(size)])
+    for T in TYPES:
+        A = arr(ref, T) if isroot else undef(1, T)
+        B = MPI.Scatterv(A, counts, root, comm)
+        check(is_array_type(B, T) and eq(B, np.full(counts[rank], rank, dtype=T)), ("scatterv", T.__name__))
+        B = undef(counts[rank], T)
+        MPI.Scatterv_(A, B, counts, root, comm)
+        check(eq(B, np.full(counts[rank], rank, dtype=T)), "scatterv!")
+        B = copy(A) if isroot else undef(counts[rank], T)
+        if isroot:
+            MPI.Scatterv_(B, None, counts, root, comm)
+            check(eq(B, host(A)), "scatterv IN_PLACE root")
+        else:
+            MPI.Scatterv_(None, B, counts, root, comm)
+            check(eq(B, np.full(counts[rank], rank, dtype=T)), ("scatterv IN_PLACE", T.__name__))
+
+
+def t_allgatherv(comm):
+    """test/test_allgatherv.jl:12-44"""
+    size, rank = MPI.Comm_size(comm), MPI.Comm_rank(comm)
+    counts = [i % 2 + 1 for i in range(size)]
+    chk = np.concatenate([np.full(counts[r], r) for r in range(size)])
+    for T in TYPES:
+        A = arr(np.full(counts[rank], rank), T)
+        B = MPI.Allgatherv(A, counts, comm)
+        check(is_array_type(B, T) and eq(B, chk.astype(T)), ("allgatherv", T.__name__))
+        B = undef(sum(counts), T)
+        MPI.Allgatherv_(A, B, counts, comm)
+        check(eq(B, chk.astype(T)), "allgatherv!")
+        B = undef(sum(counts) - 1, T)
+        raises(AssertionError, lambda: MPI.Allgatherv_(A, B, counts, comm), "allgatherv short")
+        B = arr(np.full(sum(counts), rank), T)
+        MPI.Allgatherv_(MPI.IN_PLACE, B, counts, comm)
+        check(eq(B, chk.astype(T)), ("allgatherv IN_PLACE", T.__name__))
+
+
+def t_alltoallv(comm):
+    """test/test_alltoallv.jl:12-38"""
+    size, rank = MPI.Comm_size(comm), MPI.Comm_rank(comm)
+    send_counts = list(range(1, size + 1))
+    recv_counts = [rank + 1] * size
+    send_vals = np.concatenate([np.arange(1, i + 1) for i in range(1, size + 1)])
+    recv_vals = np.concatenate([np.arange(1, rank + 2) for _ in range(size)])
+    for T in TYPES:
+        A = arr(send_vals, T)
+        B = MPI.Alltoallv(A, send_counts, recv_counts, comm)
+        check(is_array_type(B, T) and eq(B, recv_vals.astype(T)), ("alltoallv", T.__name__))
+        C = undef(sum(recv_counts), T)
+        MPI.Alltoallv_(A, C, send_counts, recv_counts, comm)
+        check(eq(C, recv_vals.astype(T)), "alltoallv!")
+        C = undef(sum(recv_counts) - 1, T)
+        raises(AssertionError, lambda: MPI.Alltoallv_(A, C, send_counts, recv_counts, comm), "alltoallv short")
+
+
 def main():
     comm = MPI.Init()
-    for t in (t_allreduce, t_reduce, t_scan, t_exscan, t_bcast, t_allgather, t_alltoall):
+    for t in (t_allreduce, t_reduce, t_scan, t_exscan, t_bcast, t_allgather, t_alltoall, t_gather, t_gatherv,
+              t_scatter, t_scatterv, t_allgatherv, t_alltoallv):
         try:
             t(comm)
         except Exception:  # noqa: BLE001

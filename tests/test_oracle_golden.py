@@ -38,9 +38,48 @@ def oracle_outputs(c, ins):
     raise KeyError(coll)
 
 
+VCOLLS = ("gather", "gatherv", "scatter", "scatterv", "allgatherv", "alltoallv")
+
+
+def v_expected(c, ins):
+    """rank -> expected output prefix for a v-collective golden case."""
+    n, seed, base, root = c["n"], c["seed"], c["count"], c["root"]
+    K = [[M.vcnt(seed, a, b, base) for b in range(16)] for a in range(16)]
+    coll = c["coll"]
+    if coll == "gather":
+        return {root: M.gather(ins, base, root)}
+    if coll == "gatherv":
+        return {root: M.gatherv(ins, [K[p][0] for p in range(n)])}
+    if coll == "scatter":
+        return dict(enumerate(M.scatter(ins[root], base, n)))
+    if coll == "scatterv":
+        return dict(enumerate(M.scatterv(ins[root], [K[p][1] for p in range(n)])))
+    if coll == "allgatherv":
+        return dict(enumerate(M.allgatherv(ins, [K[p][2] for p in range(n)])))
+    return dict(enumerate(M.alltoallv(ins, [[K[p][q] for q in range(n)] for p in range(n)])))
+
+
 GROUPS = collections.defaultdict(list)
 for _c in CASES:
-    GROUPS[(_c["coll"], _c["n"])].append(_c)
+    if _c["coll"] not in VCOLLS:
+        GROUPS[(_c["coll"], _c["n"])].append(_c)
+
+
+@pytest.mark.parametrize("coll", VCOLLS)
+def test_oracle_matches_mpich_vcollectives(coll):
+    bad, tot = [], 0
+    for c in CASES:
+        if c["coll"] != coll:
+            continue
+        dt = M.DTYPES[c["dtype"]][1]
+        ins = typed(ARR[c["id"] + ".in"], dt)
+        outs = ARR[c["id"] + ".out"]
+        for r, e in v_expected(c, ins).items():
+            tot += 1
+            got = np.ascontiguousarray(outs[r][: e.nbytes]).view(dt)
+            if not (same_bits(got, e) and (outs[r][e.nbytes:] == 0xCD).all()):
+                bad.append((c["id"], r))
+    assert tot > 0 and not bad, bad[:10]
 
 
 @pytest.mark.parametrize("key", sorted(GROUPS), ids=lambda k: f"{k[0]}-n{k[1]}")
@@ -74,7 +113,8 @@ def test_op_type_matrix_matches_oracle():
 
 def test_fixture_coverage():
     colls = {c["coll"] for c in CASES}
-    assert colls == {"reduce_local", "allreduce", "reduce", "scan", "exscan", "bcast", "allgather", "alltoall"}
+    assert colls == {"reduce_local", "allreduce", "reduce", "scan", "exscan", "bcast", "allgather", "alltoall",
+                     *VCOLLS}
     assert {c["n"] for c in CASES if c["coll"] == "allreduce"} == {2, 3, 4, 5, 6, 8}
     # the Rabenseifner regime (> 2048 B) is exercised for f32 and f64
     assert any(c["count"] * 4 > 2048 and c["dtype"] == "FLOAT" and c["coll"] == "allreduce" for c in CASES)
