@@ -50,7 +50,10 @@ struct PeerView {
   uint64_t timeout_ticks;      // wall_clock64 ticks (100 MHz) before giving up
   uint64_t* sig[kMaxRanks];    // signal array [kMaxBlocks][kMaxRanks] of every rank
   unsigned* err;               // host-visible error word (0 = ok)
-  unsigned long long* done;    // host-visible completion counter (+1 per finished block), or null
+  unsigned long long* done;    // host-visible completion word (launch sequence), or null
+  unsigned long long* dcount;  // device-memory block arrival counter (monotone)
+  unsigned long long dbase;    // dcount value before this launch
+  unsigned long long seq;      // value the last block of this launch stores to *done
   char* stage[kMaxRanks];      // staging arena base of every rank (IPC-mapped)
 };
 

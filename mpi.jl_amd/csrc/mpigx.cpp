@@ -221,7 +221,10 @@ struct mpigx_comm {
   // completion counter for blocking calls (host-pinned; kernels add 1 per block)
   volatile unsigned long long* done = nullptr;
   unsigned long long* done_dev = nullptr;
-  unsigned long long done_target = 0;
+  unsigned long long done_target = 0;  // launch sequence the host waits for
+  unsigned long long* dcount_dev = nullptr;
+  unsigned long long dcount_total = 0;  // blocks counted on dcount so far
+  unsigned long long launch_seq = 0;
   bool unflagged = false;  // work enqueued without the counter (stream-ordered mode)
   int sync_mode = 1;       // 1: spin on the counter, 0: hipStreamSynchronize
   uint64_t xseq = 0;       // host_allgather sequence
@@ -257,6 +260,9 @@ PeerView make_view(mpigx_comm* c) {
   pv.timeout_ticks = c->timeout_ticks;
   pv.err = c->err_dev;
   pv.done = (c->blocking && c->sync_mode == 1) ? c->done_dev : nullptr;
+  pv.dcount = c->dcount_dev;
+  pv.dbase = c->dcount_total;
+  pv.seq = c->launch_seq + 1;
   for (int p = 0; p < c->n; ++p) {
     pv.sig[p] = c->peer_sig[p];
     pv.stage[p] = c->peer_stage[p];
@@ -266,8 +272,13 @@ PeerView make_view(mpigx_comm* c) {
 
 // Account for one launch of `grid` blocks made with view `pv`.
 void note_launch(mpigx_comm* c, const PeerView& pv, unsigned grid) {
-  if (pv.done) c->done_target += grid;
-  else c->unflagged = true;
+  if (pv.done) {
+    c->dcount_total += grid;
+    c->launch_seq += 1;
+    c->done_target = c->launch_seq;
+  } else {
+    c->unflagged = true;
+  }
 }
 
 // After enqueueing: in blocking mode wait and translate device errors.  The
@@ -594,6 +605,8 @@ int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t*
   c->done = (volatile unsigned long long*)(c->err + 8);  // same pinned page, own 32-B slot
   HIPCK(hipHostGetDevicePointer((void**)&c->done_dev, (void*)c->done, 0));
   c->sync_mode = (int)env_ll("MPIGX_SYNC_SPIN", 1);
+  HIPCK(hipMalloc((void**)&c->dcount_dev, 64));
+  HIPCK(hipMemset(c->dcount_dev, 0, 64));
   HIPCK(hipDeviceSynchronize());
   c->peer_stage[rank] = c->stage;
   c->peer_sig[rank] = c->sig;
@@ -699,6 +712,7 @@ int mpigx_comm_free(mpigx_comm_t c) {
   if (c->shm) munmap(c->shm, sizeof(ShmBlock));
   (void)hipFree(c->stage);
   (void)hipFree(c->sig);
+  (void)hipFree(c->dcount_dev);
   (void)hipHostFree(c->err);
   delete c;
   return rc;
