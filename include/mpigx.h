@@ -195,6 +195,78 @@ int mpigx_reduce_local(const void *inbuf, void *inoutbuf, int count, int datatyp
 int mpigx_reduce_local_multi(const void *const *in, int nin, void *out, long long count,
                              int datatype, int op, int order, void *stream);
 
+/* ---- point-to-point (src/pointtopoint.jl) ----------
+ * Device buffers, rendezvous protocol: the sender publishes an envelope
+ * (tag, size, IPC handle of the allocation holding the buffer) in the
+ * receiver's shm mailbox; the receiver matches it (MPI order: per source
+ * FIFO, posted receives in post order, ANY_SOURCE / ANY_TAG) and pulls the
+ * bytes with one copy kernel on its own transfer stream, then acknowledges.
+ * Send buffers must be ready when the call is made (the comm's stream is
+ * synchronised); receive buffers are written after prior work on the comm's
+ * stream.  Progress happens inside every mpigx call on the communicator,
+ * including blocking collectives.  Requests and statuses are the MPICH ones:
+ * `int` request handles (MPIGX_REQUEST_NULL = MPI_REQUEST_NULL) and the
+ * 20-byte MPI_Status layout (mpi.h:585-591, pointtopoint.jl:4-60). */
+#define MPIGX_ERR_TAG 4
+#define MPIGX_ERR_RANK 6
+#define MPIGX_ERR_TRUNCATE 14
+#define MPIGX_ERR_IN_STATUS 17
+#define MPIGX_ERR_REQUEST 19
+#define MPIGX_ANY_SOURCE (-2)
+#define MPIGX_ANY_TAG (-1)
+#define MPIGX_PROC_NULL (-1)
+#define MPIGX_UNDEFINED (-32766)
+#define MPIGX_REQUEST_NULL 0x2c000000
+#define MPIGX_TAG_UB 0x7fffffff
+
+typedef int mpigx_request_t;
+typedef struct mpigx_status {
+  int count_lo;               /* bytes received (low 31 bits), as MPICH */
+  int count_hi_and_cancelled; /* bit 0: cancelled */
+  int MPI_SOURCE;
+  int MPI_TAG;
+  int MPI_ERROR;
+} mpigx_status_t;
+#define MPIGX_STATUS_IGNORE ((mpigx_status_t *)1)
+
+/* MPI_Send / MPI_Isend — pointtopoint.jl:188-198, :221-232 */
+int mpigx_send(const void *buf, int count, int datatype, int dest, int tag, mpigx_comm_t comm);
+int mpigx_isend(const void *buf, int count, int datatype, int dest, int tag, mpigx_comm_t comm,
+                mpigx_request_t *request);
+/* MPI_Recv / MPI_Irecv — pointtopoint.jl:266-273, :325-336 */
+int mpigx_recv(void *buf, int count, int datatype, int source, int tag, mpigx_comm_t comm,
+               mpigx_status_t *status);
+int mpigx_irecv(void *buf, int count, int datatype, int source, int tag, mpigx_comm_t comm,
+                mpigx_request_t *request);
+/* MPI_Sendrecv — pointtopoint.jl:370-386 */
+int mpigx_sendrecv(const void *sendbuf, int sendcount, int sendtype, int dest, int sendtag,
+                   void *recvbuf, int recvcount, int recvtype, int source, int recvtag,
+                   mpigx_comm_t comm, mpigx_status_t *status);
+/* MPI_Probe / MPI_Iprobe — pointtopoint.jl:107-115, :126-137 */
+int mpigx_probe(int source, int tag, mpigx_comm_t comm, mpigx_status_t *status);
+int mpigx_iprobe(int source, int tag, mpigx_comm_t comm, int *flag, mpigx_status_t *status);
+/* MPI_Get_count — pointtopoint.jl:150-156 (MPIGX_UNDEFINED if not a multiple) */
+int mpigx_get_count(const mpigx_status_t *status, int datatype, int *count);
+/* MPI_Test_cancelled */
+int mpigx_test_cancelled(const mpigx_status_t *status, int *flag);
+/* MPI_Wait / Test / Waitall / Testall / Waitany / Testany / Waitsome /
+ * Testsome / Cancel / Request_free — pointtopoint.jl:398-681.  Completed
+ * requests are freed and set to MPIGX_REQUEST_NULL; null entries are
+ * skipped and report the empty status (source ANY_SOURCE, tag ANY_TAG). */
+int mpigx_wait(mpigx_request_t *request, mpigx_status_t *status);
+int mpigx_test(mpigx_request_t *request, int *flag, mpigx_status_t *status);
+int mpigx_waitall(int count, mpigx_request_t *requests, mpigx_status_t *statuses);
+int mpigx_testall(int count, mpigx_request_t *requests, int *flag, mpigx_status_t *statuses);
+int mpigx_waitany(int count, mpigx_request_t *requests, int *index, mpigx_status_t *status);
+int mpigx_testany(int count, mpigx_request_t *requests, int *index, int *flag,
+                  mpigx_status_t *status);
+int mpigx_waitsome(int incount, mpigx_request_t *requests, int *outcount, int *indices,
+                   mpigx_status_t *statuses);
+int mpigx_testsome(int incount, mpigx_request_t *requests, int *outcount, int *indices,
+                   mpigx_status_t *statuses);
+int mpigx_cancel(mpigx_request_t *request);
+int mpigx_request_free(mpigx_request_t *request);
+
 /* ---- device buffers (north-star subsystem 1: the ROCBuffer backing) ----- */
 int mpigx_malloc(void **ptr, size_t bytes);
 int mpigx_free(void *ptr);

@@ -37,6 +37,9 @@ enum FoldMode : int {
   M_AR_TWOSHOT = 2,   // copy-in, barrier, RS (own chunk), barrier, AG, barrier
   M_RED_ONESHOT = 3,  // copy-in, barrier, root folds everything, barrier
   M_RED_TWOSHOT = 4,  // copy-in, barrier, RS (own chunk), barrier, root gathers, barrier
+  M_AR_ZC = 5,        // zero-copy two-shot: barrier, RS straight from the peers' (IPC-
+                      // registered) send buffers into my recvbuf, barrier, AG from the
+                      // peers' recvbufs, barrier
 };
 
 // Copy-kernel modes (Bcast / Allgather / Alltoall / Barrier).
@@ -81,6 +84,7 @@ struct FoldArgs {
   const void* src2[kMaxRanks];
   const void* send;    // collective modes: my send buffer (may be == recv)
   void* recv;          // output
+  char* zc_recv[kMaxRanks];  // M_AR_ZC: every rank's recvbuf (IPC-mapped; mine = recv)
 };
 
 struct CopyArgs {
@@ -116,6 +120,16 @@ struct VArgs {
   long long p_dst[kMaxRanks];  // ... into recv + p_dst[p]
   const char* send;
   char* recv;
+};
+
+// Point-to-point batch: up to kMaxXfer matched messages per launch.
+constexpr int kMaxXfer = 16;
+struct XferArgs {
+  int nseg;
+  int blk0[kMaxXfer + 1];       // first block of each segment (prefix sums)
+  char* dst[kMaxXfer];
+  const char* src[kMaxXfer];
+  long long bytes[kMaxXfer];
 };
 
 struct ScanArgs {

@@ -167,6 +167,25 @@ hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a) {
   return hipGetLastError();
 }
 
+// Point-to-point transfers (src/pointtopoint.jl): one launch moves every
+// message matched in one progress pass; segment j owns blocks
+// [blk0[j], blk0[j+1]) and is cut into equal 16-B-multiple slices.  The
+// receiver pulls from the sender's (IPC-mapped) buffer, so writes stay local.
+__global__ __launch_bounds__(kThreads) void xfer_kernel(XferArgs A) {
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < A.nseg && b >= A.blk0[j + 1]) ++j;
+  const long long g = A.blk0[j + 1] - A.blk0[j], k = b - A.blk0[j];
+  const long long slice = ((A.bytes[j] + g - 1) / g + 15) & ~15ll;
+  const long long lo = lmin(k * slice, A.bytes[j]), hi = lmin(lo + slice, A.bytes[j]);
+  block_copy(A.dst[j] + lo, A.src[j] + lo, hi - lo);
+}
+
+hipError_t launch_xfer(hipStream_t s, const XferArgs& a) {
+  hipLaunchKernelGGL(xfer_kernel, dim3(a.blk0[a.nseg]), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a) {
   if (a.pv.n <= 8)
     hipLaunchKernelGGL(copy_kernel<8>, grid, dim3(kThreads), 0, s, a);

@@ -78,6 +78,43 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
   const int es = A.esize;
   uint64_t ep = pv.epoch;
 
+  if (A.mode == M_AR_ZC) {
+    // zero-copy two-shot: no staging; sources are the peers' send buffers
+    const int n = pv.n, r = pv.rank;
+    if (!rank_barrier(pv, ep++)) return;  // every rank's send buffer is ready
+    const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+    bool vec = recv_vec;
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s)
+      if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
+#pragma unroll
+    for (int s = 0; s < NMAX / 2; ++s)
+      if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
+    fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
+    if (!rank_barrier(pv, ep++)) return;  // every reduced chunk is in its owner's recvbuf
+    char* dsts[NMAX];
+    const char* srcs[NMAX];
+    long long lens[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      dsts[j] = nullptr;
+      srcs[j] = nullptr;
+      lens[j] = 0;
+      if (j + 1 < n) {
+        const int p = (r + 1 + j) % n;
+        const long long d0 = lmin((long long)p * A.chunk, A.count), d1 = lmin(d0 + A.chunk, A.count);
+        const long long l2 = lmin(d0 + (long long)b * A.slice, d1), h2 = lmin(l2 + A.slice, d1);
+        dsts[j] = (char*)(recv + l2);
+        srcs[j] = A.zc_recv[p] + l2 * es;
+        lens[j] = (h2 - l2) * es;
+      }
+    }
+    block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    rank_barrier(pv, ep++);  // nobody reads my buffers any more
+    return;
+  }
+
   if (A.mode == M_AR_ONESHOT || A.mode == M_RED_ONESHOT) {
     const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
     block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);

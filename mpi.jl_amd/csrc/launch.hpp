@@ -22,5 +22,6 @@ MPIGX_DECL_REP(bf16)
 
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a);
 hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a);
+hipError_t launch_xfer(hipStream_t s, const XferArgs& a);
 
 }  // namespace mpigx

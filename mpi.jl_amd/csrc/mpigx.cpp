@@ -27,6 +27,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "common.hpp"
 #include "launch.hpp"
@@ -176,7 +177,7 @@ struct ShmRank {
   hipIpcMemHandle_t sig_h;
   // host control-plane exchange (host_allgather): double-buffered blobs
   std::atomic<uint64_t> xseq;
-  char xbuf[2][64];
+  char xbuf[2][256];
 };
 struct ShmBlock {
   std::atomic<uint64_t> magic;
@@ -228,6 +229,23 @@ struct mpigx_comm {
   bool unflagged = false;  // work enqueued without the counter (stream-ordered mode)
   int sync_mode = 1;       // 1: spin on the counter, 0: hipStreamSynchronize
   uint64_t xseq = 0;       // host_allgather sequence
+  // zero-copy registration caches (user buffers exported / peers' imported)
+  struct LocalReg {
+    unsigned long long id;
+    char* base;
+    hipIpcMemHandle_t h;
+  };
+  struct Import {
+    int peer;
+    unsigned long long id;
+    char* base;
+    unsigned long long tick;
+  };
+  std::vector<LocalReg> lreg;
+  std::vector<Import> imports;
+  unsigned long long tick = 0;
+  long long zc_min = 16ll << 20;  // bytes; 0 disables
+  bool zc_require = false;        // MPIGX_ZC_REQUIRE=1: error instead of the staged fallback
   // peers (index = rank; self included)
   char* peer_stage[kMaxRanks] = {};
   uint64_t* peer_sig[kMaxRanks] = {};
@@ -362,6 +380,144 @@ void plan_schedule(mpigx_comm* c, FoldArgs& a, int n, int root, long long count_
   }
 }
 
+int host_allgather(mpigx_comm* c, const void* mine, int len, void* out);
+
+// ---- zero-copy registration (large Allreduce) ------------------------------
+// A user buffer is exported by the IPC handle of the allocation that holds it
+// (hipMemGetAddressRange base) plus an offset; allocations are identified by
+// HIP's unique buffer id, so a freed-and-reused address never aliases a stale
+// import.  Peers' allocations are opened once and kept (LRU-bounded).
+constexpr size_t kZcCache = 64;
+
+struct ZcBlob {
+  int ok;
+  int pad;
+  unsigned long long id[2];
+  long long off[2];
+  hipIpcMemHandle_t h[2];
+};
+
+bool zc_export(mpigx_comm* c, const void* p, unsigned long long* id, long long* off,
+               hipIpcMemHandle_t* h) {
+  void* base = nullptr;
+  size_t size = 0;
+  unsigned long long bid = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base ||
+      hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  *id = bid;
+  *off = (const char*)p - (const char*)base;
+  for (auto& r : c->lreg)
+    if (r.id == bid && r.base == base) {
+      *h = r.h;
+      return true;
+    }
+  hipIpcMemHandle_t hh;
+  if (hipIpcGetMemHandle(&hh, base) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (c->lreg.size() >= kZcCache) c->lreg.erase(c->lreg.begin());
+  c->lreg.push_back({bid, (char*)base, hh});
+  *h = hh;
+  return true;
+}
+
+char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h) {
+  for (auto& im : c->imports)
+    if (im.peer == peer && im.id == id) {
+      im.tick = ++c->tick;
+      return im.base;
+    }
+  void* ptr = nullptr;
+  if (hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (c->imports.size() >= kZcCache) {
+    size_t oldest = 0;
+    for (size_t i = 1; i < c->imports.size(); ++i)
+      if (c->imports[i].tick < c->imports[oldest].tick) oldest = i;
+    // a queued launch of mine may still read the evicted mapping
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipIpcCloseMemHandle(c->imports[oldest].base);
+    c->imports.erase(c->imports.begin() + oldest);
+  }
+  c->imports.push_back({peer, id, (char*)ptr, ++c->tick});
+  return (char*)ptr;
+}
+
+// Resolves every rank's send/recv pointers (mapped into this process).  Two
+// host exchanges: the export descriptors, then whether every import worked,
+// so all ranks take the same path.  Returns 1 = use zero-copy, 0 = staged,
+// <0 = error code (negated).
+int zc_resolve(mpigx_comm* c, const void* send, void* recv, const char** psend, char** precv) {
+  const int n = c->n;
+  ZcBlob mine;
+  memset(&mine, 0, sizeof mine);
+  mine.ok = zc_export(c, send, &mine.id[0], &mine.off[0], &mine.h[0]) &&
+            zc_export(c, recv, &mine.id[1], &mine.off[1], &mine.h[1]);
+  static_assert(sizeof(ZcBlob) <= 256, "control-plane blob");
+  ZcBlob all[kMaxRanks];
+  int rc = host_allgather(c, &mine, sizeof mine, all);
+  if (rc) return -rc;
+  for (int q = 0; q < n; ++q)
+    if (!all[q].ok) return 0;
+  int ok = 1;
+  for (int q = 0; q < n && ok; ++q) {
+    if (q == c->rank) {
+      psend[q] = (const char*)send;
+      precv[q] = (char*)recv;
+      continue;
+    }
+    char* sb = zc_import(c, q, all[q].id[0], all[q].h[0]);
+    char* rb = all[q].id[1] == all[q].id[0] ? sb : zc_import(c, q, all[q].id[1], all[q].h[1]);
+    if (!sb || !rb) {
+      ok = 0;
+      break;
+    }
+    psend[q] = sb + all[q].off[0];
+    precv[q] = rb + all[q].off[1];
+  }
+  int oks[kMaxRanks];
+  rc = host_allgather(c, &ok, sizeof ok, oks);
+  if (rc) return -rc;
+  for (int q = 0; q < n; ++q)
+    if (!oks[q]) return 0;
+  return 1;
+}
+
+// Zero-copy two-shot Allreduce over the whole message (no rounds: nothing is
+// staged).  Same chunk/slice partition and fold schedule as M_AR_TWOSHOT.
+int allreduce_zc(mpigx_comm* c, const char* const* psend, char* const* precv, long long count,
+                 const TypeInfo* t, int oc) {
+  const int n = c->n, es = t->size;
+  const int vec = es >= 16 ? 1 : 16 / es;
+  FoldArgs a;
+  memset(&a, 0, sizeof a);
+  a.pv = make_view(c);
+  a.mode = M_AR_ZC;
+  a.esize = es;
+  a.count = count;
+  a.gbase = 0;
+  a.send = psend[c->rank];
+  a.recv = precv[c->rank];
+  for (int p = 0; p < n; ++p) a.zc_recv[p] = precv[p];
+  int nmax, sched;
+  const void* ptrs[kMaxRanks];
+  for (int p = 0; p < n; ++p) ptrs[p] = psend[p];
+  plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
+  a.chunk = rup(cdiv(count, n), vec);
+  const int grid = grid_for(c, a.chunk * es);
+  a.slice = rup(cdiv(a.chunk, grid), vec);
+  HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
+  note_launch(c, a.pv, grid);
+  c->epoch += 3;
+  return finish(c);
+}
+
 // Shared driver for Allreduce / Reduce.
 int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, const TypeInfo* t,
                   int oc, int root, bool all) {
@@ -372,6 +528,16 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   long long round = (long long)(c->stage_bytes / es);
   round = (round / (n * (long long)vec)) * n * vec;
   const char* algo_env = getenv("MPIGX_ALGO");
+  // count and the thresholds are identical on every rank, so is this test
+  if (all && n > 1 && c->zc_min > 0 && count * es >= c->zc_min &&
+      !(algo_env && !strcmp(algo_env, "oneshot"))) {
+    const char* ps[kMaxRanks];
+    char* pr[kMaxRanks];
+    const int z = zc_resolve(c, send, recv, ps, pr);
+    if (z < 0) return -z;
+    if (z == 1) return allreduce_zc(c, ps, pr, count, t, oc);
+    if (c->zc_require) return MPIGX_ERR_INTERN;  // tests: the path must not fall back
+  }
   for (long long off = 0; off < count; off += round) {
     const long long cnt = count - off < round ? count - off : round;
     FoldArgs a;
@@ -426,7 +592,7 @@ int copy_n1(mpigx_comm* c, void* dst, const void* src, size_t bytes) {
 // (double-buffered by sequence parity: a rank can only reuse a buffer after
 // every peer posted the next sequence, i.e. finished reading it).
 int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
-  if (len > 64) return MPIGX_ERR_INTERN;
+  if (len > 256) return MPIGX_ERR_INTERN;
   if (c->n == 1 || !c->shm) {
     memcpy(out, mine, len);
     return MPIGX_SUCCESS;
@@ -588,6 +754,8 @@ int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t*
   if (c->max_blocks < 1) c->max_blocks = 1;
   if (c->max_blocks > kMaxBlocks) c->max_blocks = kMaxBlocks;
   c->oneshot_max = env_ll("MPIGX_ONESHOT_MAX", 256 << 10);
+  c->zc_min = env_ll("MPIGX_ZC_MIN", 16ll << 20);
+  c->zc_require = env_ll("MPIGX_ZC_REQUIRE", 0) != 0;
   // 8 KiB of message per block: 64 KiB one-shot drops 19.5 -> 6.7 us and
   // 1 MiB two-shot 31 -> 19 us vs 64 KiB per block (tools/latency.py, 2 ranks)
   c->bytes_per_block = env_ll("MPIGX_BYTES_PER_BLOCK", 8 << 10);
@@ -709,6 +877,7 @@ int mpigx_comm_free(mpigx_comm_t c) {
     (void)hipIpcCloseMemHandle(c->peer_stage[q]);
     (void)hipIpcCloseMemHandle(c->peer_sig[q]);
   }
+  for (auto& im : c->imports) (void)hipIpcCloseMemHandle(im.base);
   if (c->shm) munmap(c->shm, sizeof(ShmBlock));
   (void)hipFree(c->stage);
   (void)hipFree(c->sig);

@@ -28,6 +28,18 @@ def test_golden_collectives(n):
     print(summ[0])
 
 
+@pytest.mark.parametrize("n", [2, 3, 5])
+def test_golden_collectives_zero_copy(n):
+    """Every Allreduce through the zero-copy path (peers read the user buffers
+    through cached hipIpc registrations; MPIGX_ZC_MIN=1 forces it at every size)."""
+    env = dict(ENV, MPIGX_ZC_MIN="1", MPIGX_ZC_REQUIRE="1")
+    rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "golden_worker.py"), n, timeout=900, extra_env=env)
+    msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
+    assert all(rc == 0 for rc in rcs), msg
+    summ = _summaries(outs)
+    assert len(summ) == n and all(x["nfail"] == 0 and x["checks"] > 200 for x in summ), summ
+
+
 def _summaries(outs):
     import json
     res = []

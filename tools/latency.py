@@ -16,7 +16,8 @@ comm = MPI.Init()
 L = MPI.lib()
 r = MPI.Comm_rank(comm)
 res = {}
-for nbytes in (8, 4096, 65536, 1 << 20, 8 << 20):
+SIZES = [int(v) for v in os.environ.get("LAT_SIZES", "8,4096,65536,1048576,8388608").split(",")]
+for nbytes in SIZES:
     x = torch.ones(nbytes // 4, device="cuda")
     y = torch.empty_like(x)
     px, py = ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr())
@@ -31,7 +32,7 @@ for nbytes in (8, 4096, 65536, 1 << 20, 8 << 20):
         torch.cuda.synchronize()
         MPI.Barrier(comm)
         t0 = time.perf_counter()
-        it = 200
+        it = 200 if nbytes <= (8 << 20) else 20
         for _ in range(it):
             if mode == "api":
                 MPI.Allreduce_(x, y, MPI.SUM, comm)

@@ -78,6 +78,30 @@ __global__ void fold8_once(P a) {
     }
   }
 }
+// wave-contiguous: each wave owns W*1 KiB contiguous of every input (lane l
+// loads l, l+64, ... inside the wave's span)
+template <int W, bool NTS>
+__global__ void fold8_wave(P a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+  const long long base = ((long long)blockIdx.x * wpb + wave) * (64 * W) + lane;
+  f32x4 v[W][8];
+#pragma unroll
+  for (int u = 0; u < W; ++u) {
+    const long long i = base + 64 * u;
+    if (i < a.nv) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[u][k] = __builtin_nontemporal_load(a.in[k] + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < W; ++u) {
+    const long long i = base + 64 * u;
+    if (i < a.nv) {
+      f32x4 r = ((v[u][0] + v[u][1]) + (v[u][2] + v[u][3])) + ((v[u][4] + v[u][5]) + (v[u][6] + v[u][7]));
+      S<NTS>(a.out + i, r);
+    }
+  }
+}
 __global__ void copyk(const f32x4* s, f32x4* d, long long nv) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x)
     __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
@@ -104,6 +128,9 @@ int main() {
   void* big; CK(hipMalloc(&big, 8 * S));  // 2 GiB single buffer for copy/read peaks
   CK(hipMemset(big, 0, 8 * S));
   std::vector<V> vs = {
+      {"wave W1 b256 plainS", 65536, 256, 20}, {"wave W2 b256 plainS", 32768, 256, 21},
+      {"wave W4 b256 plainS", 16384, 256, 22}, {"wave W2 b64 plainS", 131072, 64, 21},
+      {"wave W1 b64 plainS", 262144, 64, 20}, {"wave W4 b128 plainS", 16384*2, 128, 22},
       {"once U1 b256 NTS", 65536, 256, 10}, {"once U1 b256 staggered", 65536, 256, 14}, {"once U1 b256 plainS", 65536, 256, 11},
       {"once U2 b256 NTS", 32768, 256, 12}, {"once U4 b256 NTS", 16384, 256, 13},
       {"once U1 b512 NTS", 32768, 512, 10}, {"once U1 b1024 NTS", 16384, 1024, 10},
@@ -136,6 +163,9 @@ int main() {
           case 8: hipLaunchKernelGGL(copyk, x.grid, x.block, 0, 0, (const f32x4*)big, (f32x4*)big + 4 * nv, 4 * nv); break;
           case 9: hipLaunchKernelGGL(readk, x.grid, x.block, 0, 0, (const f32x4*)big, a.out, 8 * nv); break;
           case 10: hipLaunchKernelGGL((fold8_once<1, true>), x.grid, x.block, 0, 0, a); break;
+          case 20: hipLaunchKernelGGL((fold8_wave<1, false>), x.grid, x.block, 0, 0, a); break;
+          case 21: hipLaunchKernelGGL((fold8_wave<2, false>), x.grid, x.block, 0, 0, a); break;
+          case 22: hipLaunchKernelGGL((fold8_wave<4, false>), x.grid, x.block, 0, 0, a); break;
           case 14: hipLaunchKernelGGL((fold8_once<1, true>), x.grid, x.block, 0, 0, b); break;
           case 11: hipLaunchKernelGGL((fold8_once<1, false>), x.grid, x.block, 0, 0, a); break;
           case 12: hipLaunchKernelGGL((fold8_once<2, true>), x.grid, x.block, 0, 0, a); break;
