@@ -217,7 +217,7 @@ int mpigx_reduce_local_multi(const void *const *in, int nin, void *out, long lon
 #define MPIGX_PROC_NULL (-1)
 #define MPIGX_UNDEFINED (-32766)
 #define MPIGX_REQUEST_NULL 0x2c000000
-#define MPIGX_TAG_UB 0x7fffffff
+#define MPIGX_TAG_UB 268435455 /* MPI_TAG_UB attribute of MPICH 3.3.2 ch3 */
 
 typedef int mpigx_request_t;
 typedef struct mpigx_status {

@@ -31,6 +31,7 @@
 
 #include "common.hpp"
 #include "launch.hpp"
+#include "runtime.hpp"
 
 using namespace mpigx;
 
@@ -163,30 +164,7 @@ long long rup(long long a, long long b) { return cdiv(a, b) * b; }
 // ---------------------------------------------------------------------------
 // shm rendezvous
 // ---------------------------------------------------------------------------
-constexpr uint64_t kMagic = 0x6d70696778763031ull;  // "mpigxv01"
-
-struct ShmRank {
-  int pid;
-  int device;
-  int pci_bus;
-  int pci_dev;
-  unsigned long long stage_bytes;
-  unsigned long long stage_ptr;  // raw pointer (same-process peers)
-  unsigned long long sig_ptr;
-  hipIpcMemHandle_t stage_h;
-  hipIpcMemHandle_t sig_h;
-  // host control-plane exchange (host_allgather): double-buffered blobs
-  std::atomic<uint64_t> xseq;
-  char xbuf[2][256];
-};
-struct ShmBlock {
-  std::atomic<uint64_t> magic;
-  int nranks;
-  std::atomic<int> arrived;
-  std::atomic<int> connected;
-  std::atomic<int> failed;
-  ShmRank ranks[kMaxRanks];
-};
+// (ShmBlock / ShmRank: runtime.hpp)
 
 // Unique id payload (fits in mpigx_unique_id_t::internal).
 struct IdPayload {
@@ -202,61 +180,7 @@ double now_s() {
 
 }  // namespace
 
-// ---------------------------------------------------------------------------
-// communicator
-// ---------------------------------------------------------------------------
-struct mpigx_comm {
-  int rank = 0, n = 1, device = 0;
-  hipStream_t stream = nullptr;
-  int blocking = 1;
-  int order = MPIGX_ORDER_MPICH;
-  bool broken = false;
-  uint64_t epoch = 1;
-  uint64_t timeout_ticks = 0;
-  // local resources
-  char* stage = nullptr;
-  size_t stage_bytes = 0;
-  uint64_t* sig = nullptr;
-  unsigned* err = nullptr;  // host-pinned, device-written
-  unsigned* err_dev = nullptr;
-  // completion counter for blocking calls (host-pinned; kernels add 1 per block)
-  volatile unsigned long long* done = nullptr;
-  unsigned long long* done_dev = nullptr;
-  unsigned long long done_target = 0;  // launch sequence the host waits for
-  unsigned long long* dcount_dev = nullptr;
-  unsigned long long dcount_total = 0;  // blocks counted on dcount so far
-  unsigned long long launch_seq = 0;
-  bool unflagged = false;  // work enqueued without the counter (stream-ordered mode)
-  int sync_mode = 1;       // 1: spin on the counter, 0: hipStreamSynchronize
-  uint64_t xseq = 0;       // host_allgather sequence
-  // zero-copy registration caches (user buffers exported / peers' imported)
-  struct LocalReg {
-    unsigned long long id;
-    char* base;
-    hipIpcMemHandle_t h;
-  };
-  struct Import {
-    int peer;
-    unsigned long long id;
-    char* base;
-    unsigned long long tick;
-  };
-  std::vector<LocalReg> lreg;
-  std::vector<Import> imports;
-  unsigned long long tick = 0;
-  long long zc_min = 16ll << 20;  // bytes; 0 disables
-  bool zc_require = false;        // MPIGX_ZC_REQUIRE=1: error instead of the staged fallback
-  // peers (index = rank; self included)
-  char* peer_stage[kMaxRanks] = {};
-  uint64_t* peer_sig[kMaxRanks] = {};
-  bool peer_opened[kMaxRanks] = {};
-  ShmBlock* shm = nullptr;
-  // tuning
-  int max_blocks = 256;
-  long long oneshot_max = 256 << 10;
-  long long bytes_per_block = 64 << 10;
-  std::mutex mu;
-};
+// (struct mpigx_comm: runtime.hpp)
 
 namespace {
 
@@ -314,6 +238,9 @@ int finish(mpigx_comm* c) {
     const double limit = c->timeout_ticks / 1e8 + 5.0;
     unsigned spins = 0;
     while (*c->done < c->done_target) {
+      // keep point-to-point rendezvous moving while blocked here (a peer may
+      // wait on our acknowledgement before it joins this collective)
+      if (c->p2p && (spins & 63) == 0) rt::p2p_progress(c);
       if ((++spins & 1023) == 0 && now_s() - t0 > limit) {
         HIPCK(hipStreamSynchronize(c->stream));
         c->done_target = *c->done;
@@ -442,6 +369,7 @@ char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemH
       if (c->imports[i].tick < c->imports[oldest].tick) oldest = i;
     // a queued launch of mine may still read the evicted mapping
     (void)hipStreamSynchronize(c->stream);
+    rt::p2p_sync(c);
     (void)hipIpcCloseMemHandle(c->imports[oldest].base);
     c->imports.erase(c->imports.begin() + oldest);
   }
@@ -605,6 +533,7 @@ int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
   for (int q = 0; q < c->n; ++q) {
     unsigned spins = 0;
     while (c->shm->ranks[q].xseq.load(std::memory_order_acquire) < k) {
+      if (c->p2p && (spins & 63) == 0) rt::p2p_progress(c);
       if ((++spins & 4095) == 0 && now_s() - t0 > limit) {
         c->broken = true;
         return MPIGX_ERR_OTHER;
@@ -674,6 +603,24 @@ int vexchange(mpigx_comm* c, const VSpec& s) {
 }
 
 }  // namespace
+
+// Runtime services for p2p.cpp (runtime.hpp).
+namespace mpigx {
+namespace rt {
+int comm_check(mpigx_comm* c) { return check_comm(c); }
+int dtype_size(int datatype) {
+  const TypeInfo* t = find_type(datatype);
+  return t ? t->size : -1;
+}
+bool export_buf(mpigx_comm* c, const void* p, unsigned long long* id, long long* off, hipIpcMemHandle_t* h) {
+  return zc_export(c, p, id, off, h);
+}
+char* import_buf(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h) {
+  return zc_import(c, peer, id, h);
+}
+double wall() { return now_s(); }
+}  // namespace rt
+}  // namespace mpigx
 
 // ===========================================================================
 // C ABI
@@ -872,6 +819,7 @@ int mpigx_comm_free(mpigx_comm_t c) {
     c->blocking = b;
   }
   (void)hipStreamSynchronize(c->stream);
+  rt::p2p_destroy(c);
   for (int q = 0; q < c->n; ++q) {
     if (!c->peer_opened[q]) continue;
     (void)hipIpcCloseMemHandle(c->peer_stage[q]);

@@ -1,0 +1,140 @@
+// runtime.hpp — host-runtime internals shared by mpigx.cpp (communicators,
+// collectives) and p2p.cpp (point-to-point): the shm rendezvous block, the
+// communicator object and the few helpers both sides call.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <mutex>
+#include <vector>
+
+#include "common.hpp"
+
+namespace mpigx {
+
+// ---------------------------------------------------------------------------
+// shm block (one per communicator, mapped by every rank)
+// ---------------------------------------------------------------------------
+constexpr uint64_t kMagic = 0x6d70696778763032ull;  // "mpigxv02"
+
+struct ShmRank {
+  int pid;
+  int device;
+  int pci_bus;
+  int pci_dev;
+  unsigned long long stage_bytes;
+  unsigned long long stage_ptr;  // raw pointer (same-process peers)
+  unsigned long long sig_ptr;
+  hipIpcMemHandle_t stage_h;
+  hipIpcMemHandle_t sig_h;
+  // host control-plane exchange (host_allgather): double-buffered blobs
+  std::atomic<uint64_t> xseq;
+  char xbuf[2][256];
+};
+
+// Point-to-point envelope: written by the sender into the (sender, receiver)
+// mailbox, consumed in order by the receiver.  `posted` = message seq + 1
+// once the fields are valid; `done` = seq + 1 once the receiver has pulled
+// the bytes (the slot may then be reused and the send request completes).
+constexpr int kP2PSlots = 32;
+struct alignas(64) P2PEnvelope {
+  std::atomic<uint64_t> posted;
+  std::atomic<uint64_t> done;
+  int tag;
+  int pad;
+  long long bytes;
+  unsigned long long buf_id;     // HIP buffer id of the allocation holding the data
+  long long off;                 // offset of the data in that allocation
+  unsigned long long raw;        // sender's own pointer (self-sends)
+  hipIpcMemHandle_t h;           // IPC handle of the allocation
+};
+struct P2PMailbox {
+  P2PEnvelope slot[kP2PSlots];
+};
+
+struct ShmBlock {
+  std::atomic<uint64_t> magic;
+  int nranks;
+  std::atomic<int> arrived;
+  std::atomic<int> connected;
+  std::atomic<int> failed;
+  ShmRank ranks[kMaxRanks];
+  P2PMailbox box[kMaxRanks][kMaxRanks];  // [sender][receiver]
+};
+
+struct P2PState;  // p2p.cpp
+
+}  // namespace mpigx
+
+// ---------------------------------------------------------------------------
+// communicator
+// ---------------------------------------------------------------------------
+struct mpigx_comm {
+  int rank = 0, n = 1, device = 0;
+  hipStream_t stream = nullptr;
+  int blocking = 1;
+  int order = MPIGX_ORDER_MPICH;
+  bool broken = false;
+  uint64_t epoch = 1;
+  uint64_t timeout_ticks = 0;
+  // local resources
+  char* stage = nullptr;
+  size_t stage_bytes = 0;
+  uint64_t* sig = nullptr;
+  unsigned* err = nullptr;  // host-pinned, device-written
+  unsigned* err_dev = nullptr;
+  // completion counter for blocking calls (host-pinned; kernels add 1 per block)
+  volatile unsigned long long* done = nullptr;
+  unsigned long long* done_dev = nullptr;
+  unsigned long long done_target = 0;  // launch sequence the host waits for
+  unsigned long long* dcount_dev = nullptr;
+  unsigned long long dcount_total = 0;  // blocks counted on dcount so far
+  unsigned long long launch_seq = 0;
+  bool unflagged = false;  // work enqueued without the counter (stream-ordered mode)
+  int sync_mode = 1;       // 1: spin on the counter, 0: hipStreamSynchronize
+  uint64_t xseq = 0;       // host_allgather sequence
+  // zero-copy registration caches (user buffers exported / peers' imported)
+  struct LocalReg {
+    unsigned long long id;
+    char* base;
+    hipIpcMemHandle_t h;
+  };
+  struct Import {
+    int peer;
+    unsigned long long id;
+    char* base;
+    unsigned long long tick;
+  };
+  std::vector<LocalReg> lreg;
+  std::vector<Import> imports;
+  unsigned long long tick = 0;
+  long long zc_min = 16ll << 20;  // bytes; 0 disables
+  bool zc_require = false;        // MPIGX_ZC_REQUIRE=1: error instead of the staged fallback
+  // peers (index = rank; self included)
+  char* peer_stage[mpigx::kMaxRanks] = {};
+  uint64_t* peer_sig[mpigx::kMaxRanks] = {};
+  bool peer_opened[mpigx::kMaxRanks] = {};
+  mpigx::ShmBlock* shm = nullptr;
+  // point-to-point engine (created on first use)
+  mpigx::P2PState* p2p = nullptr;
+  // tuning
+  int max_blocks = 256;
+  long long oneshot_max = 256 << 10;
+  long long bytes_per_block = 64 << 10;
+  std::mutex mu;
+};
+
+namespace mpigx {
+namespace rt {
+// mpigx.cpp
+int comm_check(mpigx_comm* c);
+int dtype_size(int datatype);  // bytes, or -1 if not a valid datatype handle
+bool export_buf(mpigx_comm* c, const void* p, unsigned long long* id, long long* off, hipIpcMemHandle_t* h);
+char* import_buf(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h);
+double wall();
+// p2p.cpp
+void p2p_progress(mpigx_comm* c);
+void p2p_sync(mpigx_comm* c);     // drain the transfer stream
+void p2p_destroy(mpigx_comm* c);
+}  // namespace rt
+}  // namespace mpigx

@@ -165,6 +165,126 @@ for (jl, c) in ((:Scan!, :mpigx_scan), (:Exscan!, :mpigx_exscan))
     end
 end
 
+# ---------------------------------------------------------------------------
+# point-to-point (src/pointtopoint.jl) on device buffers.  libmpigx requests
+# are MPICH-style Cint handles; they live in their own type so Wait!/Test!
+# dispatch to libmpigx without overwriting MPI.jl's Request methods.
+# ---------------------------------------------------------------------------
+import MPI: Send, Isend, Recv!, Irecv!, Sendrecv!, Wait!, Test!, Waitall!, Testall!, Waitany!,
+            Cancel!, Buffer, Status, MPI_Request, STATUS_EMPTY
+
+const DevBuffer = Buffer{<:ROCBuffer}
+const MPIGX_REQUEST_NULL = Cint(0x2c000000)
+const MPIGX_UNDEFINED = Cint(-32766)
+
+mutable struct ROCRequest
+    val::Cint
+    buffer::Any
+end
+ROCRequest() = ROCRequest(MPIGX_REQUEST_NULL, nothing)
+isnull(r::ROCRequest) = r.val == MPIGX_REQUEST_NULL
+function free(r::ROCRequest)
+    if !isnull(r)
+        ccall((:mpigx_request_free, libmpigx), Cint, (Ptr{Cint},), Ref(r.val))
+        r.val = MPIGX_REQUEST_NULL
+        r.buffer = nothing
+    end
+end
+
+# pointtopoint.jl:188-198
+function Send(buf::DevBuffer, dest::Integer, tag::Integer, comm::Comm)
+    @mpichk ccall((:mpigx_send, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, Cint, Cint, Ptr{Cvoid}),
+                  buf.data, buf.count, buf.datatype, dest, tag, engine(comm))
+    nothing
+end
+# pointtopoint.jl:221-236
+function Isend(buf::DevBuffer, dest::Integer, tag::Integer, comm::Comm)
+    h = Ref{Cint}(MPIGX_REQUEST_NULL)
+    @mpichk ccall((:mpigx_isend, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, Cint, Cint, Ptr{Cvoid}, Ptr{Cint}),
+                  buf.data, buf.count, buf.datatype, dest, tag, engine(comm), h)
+    req = ROCRequest(h[], buf)
+    finalizer(free, req)
+    req
+end
+# pointtopoint.jl:266-276
+function Recv!(buf::DevBuffer, src::Integer, tag::Integer, comm::Comm)
+    stat_ref = Ref{Status}(STATUS_EMPTY)
+    @mpichk ccall((:mpigx_recv, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, Cint, Cint, Ptr{Cvoid}, Ptr{Status}),
+                  buf.data, buf.count, buf.datatype, src, tag, engine(comm), stat_ref)
+    stat_ref[]
+end
+# pointtopoint.jl:325-339
+function Irecv!(buf::DevBuffer, src::Integer, tag::Integer, comm::Comm)
+    h = Ref{Cint}(MPIGX_REQUEST_NULL)
+    @mpichk ccall((:mpigx_irecv, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, Cint, Cint, Ptr{Cvoid}, Ptr{Cint}),
+                  buf.data, buf.count, buf.datatype, src, tag, engine(comm), h)
+    req = ROCRequest(h[], buf)
+    finalizer(free, req)
+    req
+end
+# pointtopoint.jl:370-391
+function Sendrecv!(sendbuf::DevBuffer, dest::Integer, sendtag::Integer,
+                   recvbuf::DevBuffer, source::Integer, recvtag::Integer, comm::Comm)
+    stat_ref = Ref{Status}(STATUS_EMPTY)
+    @mpichk ccall((:mpigx_sendrecv, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, Cint, Cint, MPIPtr, Cint, MPI_Datatype, Cint, Cint,
+                   Ptr{Cvoid}, Ptr{Status}),
+                  sendbuf.data, sendbuf.count, sendbuf.datatype, dest, sendtag,
+                  recvbuf.data, recvbuf.count, recvbuf.datatype, source, recvtag, engine(comm), stat_ref)
+    stat_ref[]
+end
+# pointtopoint.jl:398-417 (returns the Status; the reference returns `stat`, a typo)
+function Wait!(req::ROCRequest)
+    stat_ref = Ref{Status}(STATUS_EMPTY)
+    h = Ref(req.val)
+    @mpichk ccall((:mpigx_wait, libmpigx), Cint, (Ptr{Cint}, Ptr{Status}), h, stat_ref)
+    req.val = h[]; req.buffer = nothing
+    stat_ref[]
+end
+# pointtopoint.jl:427-446
+function Test!(req::ROCRequest)
+    flag = Ref{Cint}(0); stat_ref = Ref{Status}(STATUS_EMPTY); h = Ref(req.val)
+    @mpichk ccall((:mpigx_test, libmpigx), Cint, (Ptr{Cint}, Ptr{Cint}, Ptr{Status}), h, flag, stat_ref)
+    flag[] == 0 && return (false, nothing)
+    req.val = h[]; req.buffer = nothing
+    (true, stat_ref[])
+end
+# pointtopoint.jl:457-477
+function Waitall!(reqs::Vector{ROCRequest})
+    vals = [r.val for r in reqs]; stats = fill(STATUS_EMPTY, length(reqs))
+    @mpichk ccall((:mpigx_waitall, libmpigx), Cint, (Cint, Ptr{Cint}, Ptr{Status}), length(reqs), vals, stats)
+    for (r, v) in zip(reqs, vals); r.val = v; r.buffer = nothing; end
+    stats
+end
+# pointtopoint.jl:490-514
+function Testall!(reqs::Vector{ROCRequest})
+    vals = [r.val for r in reqs]; flag = Ref{Cint}(0); stats = fill(STATUS_EMPTY, length(reqs))
+    @mpichk ccall((:mpigx_testall, libmpigx), Cint, (Cint, Ptr{Cint}, Ptr{Cint}, Ptr{Status}),
+                  length(reqs), vals, flag, stats)
+    flag[] == 0 && return (false, nothing)
+    for (r, v) in zip(reqs, vals); r.val = v; r.buffer = nothing; end
+    (true, stats)
+end
+# pointtopoint.jl:527-546
+function Waitany!(reqs::Vector{ROCRequest})
+    vals = [r.val for r in reqs]; ind = Ref{Cint}(); stat_ref = Ref{Status}(STATUS_EMPTY)
+    @mpichk ccall((:mpigx_waitany, libmpigx), Cint, (Cint, Ptr{Cint}, Ptr{Cint}, Ptr{Status}),
+                  length(reqs), vals, ind, stat_ref)
+    ind[] == MPIGX_UNDEFINED && return (0, stat_ref[])
+    i = Int(ind[]) + 1
+    reqs[i].val = vals[i]; reqs[i].buffer = nothing
+    (i, stat_ref[])
+end
+# pointtopoint.jl:671-681
+function Cancel!(req::ROCRequest)
+    @mpichk ccall((:mpigx_cancel, libmpigx), Cint, (Ptr{Cint},), Ref(req.val))
+    nothing
+end
+
 function __finalize()
     for h in values(ENGINE)
         ccall((:mpigx_comm_free, libmpigx), Cint, (Ptr{Cvoid},), h)
@@ -177,6 +297,6 @@ end
 # finalizer runs after them (environment.jl:37-62, refcount_inc/_dec).
 atexit(__finalize)
 
-export ROCBuffer
+export ROCBuffer, ROCRequest
 
 end # module

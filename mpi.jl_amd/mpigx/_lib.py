@@ -59,6 +59,27 @@ PROTOTYPES = {
     "mpigx_reduce_local": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int]),
     "mpigx_reduce_local_multi": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_longlong, c_int, c_int, c_int,
                                          c_void_p]),
+    # point-to-point
+    "mpigx_send": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "mpigx_isend": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, _IP]),
+    "mpigx_recv": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "mpigx_irecv": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, _IP]),
+    "mpigx_sendrecv": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                               c_void_p, c_void_p]),
+    "mpigx_probe": (c_int, [c_int, c_int, c_void_p, c_void_p]),
+    "mpigx_iprobe": (c_int, [c_int, c_int, c_void_p, _IP, c_void_p]),
+    "mpigx_get_count": (c_int, [c_void_p, c_int, _IP]),
+    "mpigx_test_cancelled": (c_int, [c_void_p, _IP]),
+    "mpigx_wait": (c_int, [_IP, c_void_p]),
+    "mpigx_test": (c_int, [_IP, _IP, c_void_p]),
+    "mpigx_waitall": (c_int, [c_int, _IP, c_void_p]),
+    "mpigx_testall": (c_int, [c_int, _IP, _IP, c_void_p]),
+    "mpigx_waitany": (c_int, [c_int, _IP, _IP, c_void_p]),
+    "mpigx_testany": (c_int, [c_int, _IP, _IP, _IP, c_void_p]),
+    "mpigx_waitsome": (c_int, [c_int, _IP, _IP, _IP, c_void_p]),
+    "mpigx_testsome": (c_int, [c_int, _IP, _IP, _IP, c_void_p]),
+    "mpigx_cancel": (c_int, [_IP]),
+    "mpigx_request_free": (c_int, [_IP]),
     "mpigx_malloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),
     "mpigx_free": (c_int, [c_void_p]),
     "mpigx_memcpy": (c_int, [c_void_p, c_void_p, c_size_t]),

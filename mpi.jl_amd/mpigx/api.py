@@ -58,6 +58,16 @@ def _check(rc: int):
         raise MPIError(rc)
 
 
+def Error_class(code: int) -> int:
+    """MPI_Error_class.  libmpigx returns classes already (and a class is
+    its own code); host libmpi codes are decoded by libmpi."""
+    if _state["host"]:
+        out = ctypes.c_int()
+        hostmpi.lib().MPI_Error_class(int(code), ctypes.byref(out))
+        return out.value
+    return int(code)
+
+
 # ---------------------------------------------------------------------------
 # Datatype (src/datatypes.jl:16-60, 269-292)
 # ---------------------------------------------------------------------------
