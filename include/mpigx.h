@@ -31,6 +31,7 @@ extern "C" {
 #define MPIGX_VERSION_MINOR 1
 
 #define MPIGX_MAX_RANKS 16
+#define MPIGX_UNDEFINED (-32766) /* MPI_UNDEFINED */
 
 /* ---- error classes: identical to MPICH's (mpi.h:782-809) ---------------- */
 #define MPIGX_SUCCESS 0
@@ -120,6 +121,9 @@ int mpigx_get_unique_id(mpigx_unique_id_t *id);
 int mpigx_comm_init_rank(mpigx_comm_t *comm, int nranks, const mpigx_unique_id_t *id,
                          int rank, int device);
 int mpigx_comm_free(mpigx_comm_t comm);
+/* MPI_Comm_split — comm.jl:92-105.  Collective; color = MPIGX_UNDEFINED
+ * (-32766) gives *newcomm = NULL.  Members keep the parent's device. */
+int mpigx_comm_split(mpigx_comm_t comm, int color, int key, mpigx_comm_t *newcomm);
 int mpigx_comm_rank(mpigx_comm_t comm, int *rank);
 int mpigx_comm_size(mpigx_comm_t comm, int *size);
 int mpigx_comm_device(mpigx_comm_t comm, int *device);
@@ -215,7 +219,6 @@ int mpigx_reduce_local_multi(const void *const *in, int nin, void *out, long lon
 #define MPIGX_ANY_SOURCE (-2)
 #define MPIGX_ANY_TAG (-1)
 #define MPIGX_PROC_NULL (-1)
-#define MPIGX_UNDEFINED (-32766)
 #define MPIGX_REQUEST_NULL 0x2c000000
 #define MPIGX_TAG_UB 268435455 /* MPI_TAG_UB attribute of MPICH 3.3.2 ch3 */
 
@@ -266,6 +269,85 @@ int mpigx_testsome(int incount, mpigx_request_t *requests, int *outcount, int *i
                    mpigx_status_t *statuses);
 int mpigx_cancel(mpigx_request_t *request);
 int mpigx_request_free(mpigx_request_t *request);
+
+/* ---- one-sided communication (src/onesided.jl) -----
+ * Windows over device memory.  Get is pulled by the origin straight from the
+ * target's (IPC-mapped) window; Put / Accumulate / Get_accumulate /
+ * Fetch_and_op are posted as envelopes to the target, which applies them to
+ * its own memory — pulling the origin buffer over xGMI with the op fused into
+ * the pull — so only the GPU that owns a window ever writes it (the same
+ * coherence rule as the collectives).  Consequence, as for MPICH ch3 on
+ * non-shared windows: passive-target operations complete when the target
+ * makes progress, i.e. is inside any mpigx call on the communicator
+ * (blocking collectives, Wait, Barrier, Win_* ...).  Accumulates to one
+ * target are applied in one stream, so they are atomic per element and
+ * ordered per origin, as MPI requires.  Operand roles: window = inout,
+ * origin = in (MPICH's MPI_Accumulate), pinned by tests/golden/rma_golden.json.
+ * Handles are opaque pointers (MPI.jl's Win wraps MPI_Win the same way,
+ * onesided.jl:1-3); errors are MPI error classes. */
+#define MPIGX_ERR_WIN 45
+#define MPIGX_ERR_BASE 46
+#define MPIGX_ERR_LOCKTYPE 47
+#define MPIGX_ERR_RMA_SYNC 50
+#define MPIGX_ERR_SIZE 51
+#define MPIGX_ERR_DISP 52
+#define MPIGX_ERR_RMA_RANGE 55
+#define MPIGX_ERR_RMA_ATTACH 56
+#define MPIGX_ERR_RMA_FLAVOR 58
+#define MPIGX_REPLACE 1476395021 /* MPI_REPLACE (mpi.h:322) */
+#define MPIGX_NO_OP 1476395022   /* MPI_NO_OP   (mpi.h:323) */
+#define MPIGX_LOCK_EXCLUSIVE 234
+#define MPIGX_LOCK_SHARED 235
+#define MPIGX_MODE_NOCHECK 1024
+#define MPIGX_WIN_FLAVOR_CREATE 1
+#define MPIGX_WIN_FLAVOR_ALLOCATE 2 /* (not produced) */
+#define MPIGX_WIN_FLAVOR_DYNAMIC 3
+#define MPIGX_WIN_FLAVOR_SHARED 4
+
+typedef struct mpigx_win *mpigx_win_t;
+
+/* MPI_Win_create — onesided.jl:24-34 (base: device pointer; size in bytes) */
+int mpigx_win_create(void *base, long long size, int disp_unit, mpigx_comm_t comm, mpigx_win_t *win);
+/* MPI_Win_create_dynamic — onesided.jl:47-56 */
+int mpigx_win_create_dynamic(mpigx_comm_t comm, mpigx_win_t *win);
+/* MPI_Win_allocate_shared — onesided.jl:72-83: device memory owned by this
+ * rank (uncached HBM, zero-filled), IPC-mapped by every peer */
+int mpigx_win_allocate_shared(long long size, int disp_unit, mpigx_comm_t comm, void *baseptr,
+                              mpigx_win_t *win);
+/* MPI_Win_shared_query — onesided.jl:98-108 (baseptr: this process's mapping
+ * of `rank`'s segment; rank = MPIGX_PROC_NULL: first non-empty segment) */
+int mpigx_win_shared_query(mpigx_win_t win, int rank, long long *size, int *disp_unit, void *baseptr);
+/* MPI_Win_free — onesided.jl:85-92 (collective; *win set to NULL) */
+int mpigx_win_free(mpigx_win_t *win);
+/* MPI_Win_attach / MPI_Win_detach — onesided.jl:110-122 (dynamic windows:
+ * target_disp is the absolute device address, MPI_Get_address) */
+int mpigx_win_attach(mpigx_win_t win, void *base, long long size);
+int mpigx_win_detach(mpigx_win_t win, const void *base);
+/* MPI_Win_fence / flush / sync / lock / unlock — onesided.jl:124-148 */
+int mpigx_win_fence(int assert_, mpigx_win_t win);
+int mpigx_win_flush(int rank, mpigx_win_t win);
+int mpigx_win_sync(mpigx_win_t win);
+int mpigx_win_lock(int lock_type, int rank, int assert_, mpigx_win_t win);
+int mpigx_win_unlock(int rank, mpigx_win_t win);
+/* MPI_Win_get_attr(MPI_WIN_CREATE_FLAVOR) analogue */
+int mpigx_win_get_flavor(mpigx_win_t win, int *flavor);
+/* MPI_Get / MPI_Put — onesided.jl:150-184 */
+int mpigx_get(void *origin_addr, int origin_count, int origin_datatype, int target_rank,
+              long long target_disp, int target_count, int target_datatype, mpigx_win_t win);
+int mpigx_put(const void *origin_addr, int origin_count, int origin_datatype, int target_rank,
+              long long target_disp, int target_count, int target_datatype, mpigx_win_t win);
+/* MPI_Fetch_and_op — onesided.jl:186-195 */
+int mpigx_fetch_and_op(const void *origin_addr, void *result_addr, int datatype, int target_rank,
+                       long long target_disp, int op, mpigx_win_t win);
+/* MPI_Accumulate — onesided.jl:197-206 */
+int mpigx_accumulate(const void *origin_addr, int origin_count, int origin_datatype, int target_rank,
+                     long long target_disp, int target_count, int target_datatype, int op,
+                     mpigx_win_t win);
+/* MPI_Get_accumulate — onesided.jl:208-219 */
+int mpigx_get_accumulate(const void *origin_addr, int origin_count, int origin_datatype,
+                         void *result_addr, int result_count, int result_datatype, int target_rank,
+                         long long target_disp, int target_count, int target_datatype, int op,
+                         mpigx_win_t win);
 
 /* ---- device buffers (north-star subsystem 1: the ROCBuffer backing) ----- */
 int mpigx_malloc(void **ptr, size_t bytes);

@@ -27,6 +27,10 @@ enum OpCode : int {
   O_NONE = -1
 };
 
+// RMA-only ops (MPI_REPLACE / MPI_NO_OP, mpi.h:322-323): accumulate kernels only.
+constexpr int O_REPLACE = 16;
+constexpr int O_NOOP = 17;
+
 // Fold schedule (template parameter of the fold kernels).
 enum Sched : int { S_TREE = 0, S_LINEAR = 1 };
 
@@ -130,6 +134,17 @@ struct XferArgs {
   char* dst[kMaxXfer];
   const char* src[kMaxXfer];
   long long bytes[kMaxXfer];
+};
+
+// RMA accumulate applied by the TARGET to its own window memory (rma.cpp):
+//   res[i] = dst[i] (Get_accumulate / Fetch_and_op), dst[i] = OP(dst[i], src[i])
+// with dst = inout (the target) and src = in (the origin's buffer, pulled over
+// xGMI), MPICH's operand roles for MPI_Accumulate.
+struct AccArgs {
+  const void* src;
+  void* dst;
+  void* res;  // may be null
+  long long count;
 };
 
 struct ScanArgs {

@@ -34,6 +34,11 @@ hipError_t scan_op(dim3 grid, hipStream_t s, const ScanArgs& a) {
   hipLaunchKernelGGL((scan_kernel<OP, T>), grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
+template <class OP>
+hipError_t acc_op(dim3 grid, hipStream_t s, const AccArgs& a) {
+  hipLaunchKernelGGL((acc_kernel<OP, T>), grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
 }  // namespace
 
 hipError_t MPIGX_CAT(launch_fold_, MPIGX_REP_NAME)(int op, int nmax, int sched, dim3 grid, hipStream_t s,
@@ -85,6 +90,36 @@ hipError_t MPIGX_CAT(launch_scan_, MPIGX_REP_NAME)(int op, dim3 grid, hipStream_
       case O_BAND: return scan_op<OpBand>(grid, s, a);
       case O_BOR: return scan_op<OpBor>(grid, s, a);
       case O_BXOR: return scan_op<OpBxor>(grid, s, a);
+      default: break;
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+// RMA accumulate: the collective op set plus REPLACE / NO_OP (any type).
+hipError_t MPIGX_CAT(launch_acc_, MPIGX_REP_NAME)(int op, dim3 grid, hipStream_t s, const AccArgs& a) {
+  switch (op) {
+    case O_REPLACE: return acc_op<OpReplace>(grid, s, a);
+    case O_NOOP: return acc_op<OpNoop>(grid, s, a);
+    case O_SUM: return acc_op<OpSum>(grid, s, a);
+    case O_PROD: return acc_op<OpProd>(grid, s, a);
+    default: break;
+  }
+  if constexpr (!kCplx) {
+    switch (op) {
+      case O_MIN: return acc_op<OpMin>(grid, s, a);
+      case O_MAX: return acc_op<OpMax>(grid, s, a);
+      case O_LAND: return acc_op<OpLand>(grid, s, a);
+      case O_LOR: return acc_op<OpLor>(grid, s, a);
+      case O_LXOR: return acc_op<OpLxor>(grid, s, a);
+      default: break;
+    }
+  }
+  if constexpr (kInt) {
+    switch (op) {
+      case O_BAND: return acc_op<OpBand>(grid, s, a);
+      case O_BOR: return acc_op<OpBor>(grid, s, a);
+      case O_BXOR: return acc_op<OpBxor>(grid, s, a);
       default: break;
     }
   }

@@ -272,3 +272,46 @@ __device__ __forceinline__ void scan_body(const ScanArgs& A) {
 }
 
 }  // namespace mpigx
+
+namespace mpigx {
+
+// ---------------------------------------------------------------------------
+// acc_kernel<OP,T>: RMA Accumulate / Get_accumulate / Fetch_and_op applied by
+// the target rank to its own window (rma.cpp) — the origin's data is pulled
+// over xGMI and the op is fused into the pull, so the only GPU writing the
+// window is the one that owns it.  res (old values) is target-local scratch.
+// ---------------------------------------------------------------------------
+struct OpReplace { static constexpr int code = O_REPLACE; };
+struct OpNoop { static constexpr int code = O_NOOP; };
+
+template <class OP, class T>
+__global__ __launch_bounds__(kThreads) void acc_kernel(AccArgs A) {
+  const T* __restrict__ src = reinterpret_cast<const T*>(A.src);
+  T* __restrict__ dst = reinterpret_cast<T*>(A.dst);
+  T* __restrict__ res = reinterpret_cast<T*>(A.res);
+  const long long n = A.count, nt = (long long)gridDim.x * blockDim.x;
+  constexpr int U = 4;  // independent elements in flight per thread
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * nt < n; i += U * nt) {
+    T t[U], s[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      t[u] = dst[i + u * nt];
+      if constexpr (OP::code != O_NOOP) s[u] = src[i + u * nt];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (res) res[i + u * nt] = t[u];
+      if constexpr (OP::code == O_REPLACE) dst[i + u * nt] = s[u];
+      else if constexpr (OP::code != O_NOOP) dst[i + u * nt] = OP::apply(t[u], s[u]);
+    }
+  }
+  for (; i < n; i += nt) {
+    const T t = dst[i];
+    if (res) res[i] = t;
+    if constexpr (OP::code == O_REPLACE) dst[i] = src[i];
+    else if constexpr (OP::code != O_NOOP) dst[i] = OP::apply(t, src[i]);
+  }
+}
+
+}  // namespace mpigx

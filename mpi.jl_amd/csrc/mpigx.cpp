@@ -240,7 +240,7 @@ int finish(mpigx_comm* c) {
     while (*c->done < c->done_target) {
       // keep point-to-point rendezvous moving while blocked here (a peer may
       // wait on our acknowledgement before it joins this collective)
-      if (c->p2p && (spins & 63) == 0) rt::p2p_progress(c);
+      if ((spins & 63) == 0) rt::progress_all(c);
       if ((++spins & 1023) == 0 && now_s() - t0 > limit) {
         HIPCK(hipStreamSynchronize(c->stream));
         c->done_target = *c->done;
@@ -364,16 +364,19 @@ char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemH
     return nullptr;
   }
   if (c->imports.size() >= kZcCache) {
-    size_t oldest = 0;
-    for (size_t i = 1; i < c->imports.size(); ++i)
-      if (c->imports[i].tick < c->imports[oldest].tick) oldest = i;
-    // a queued launch of mine may still read the evicted mapping
-    (void)hipStreamSynchronize(c->stream);
-    rt::p2p_sync(c);
-    (void)hipIpcCloseMemHandle(c->imports[oldest].base);
-    c->imports.erase(c->imports.begin() + oldest);
+    long oldest = -1;
+    for (size_t i = 0; i < c->imports.size(); ++i)
+      if (c->imports[i].pins == 0 && (oldest < 0 || c->imports[i].tick < c->imports[oldest].tick)) oldest = (long)i;
+    if (oldest >= 0) {
+      // a queued launch of mine may still read the evicted mapping
+      (void)hipStreamSynchronize(c->stream);
+      rt::p2p_sync(c);
+      rt::rma_sync(c);
+      (void)hipIpcCloseMemHandle(c->imports[oldest].base);
+      c->imports.erase(c->imports.begin() + oldest);
+    }
   }
-  c->imports.push_back({peer, id, (char*)ptr, ++c->tick});
+  c->imports.push_back({peer, id, (char*)ptr, ++c->tick, 0});
   return (char*)ptr;
 }
 
@@ -533,7 +536,7 @@ int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
   for (int q = 0; q < c->n; ++q) {
     unsigned spins = 0;
     while (c->shm->ranks[q].xseq.load(std::memory_order_acquire) < k) {
-      if (c->p2p && (spins & 63) == 0) rt::p2p_progress(c);
+      if ((spins & 63) == 0) rt::progress_all(c);
       if ((++spins & 4095) == 0 && now_s() - t0 > limit) {
         c->broken = true;
         return MPIGX_ERR_OTHER;
@@ -617,6 +620,45 @@ bool export_buf(mpigx_comm* c, const void* p, unsigned long long* id, long long*
 }
 char* import_buf(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h) {
   return zc_import(c, peer, id, h);
+}
+char* import_pinned(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h) {
+  char* p = zc_import(c, peer, id, h);
+  if (p)
+    for (auto& im : c->imports)
+      if (im.base == p) ++im.pins;
+  return p;
+}
+void unpin(mpigx_comm* c, char* base) {
+  for (auto& im : c->imports)
+    if (im.base == base && im.pins > 0) {
+      --im.pins;
+      return;
+    }
+}
+int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
+  return ::host_allgather(c, mine, len, out);
+}
+int acc_check(int datatype, int op, int* rep, int* esize, int* oc) {
+  const TypeInfo* t = find_type(datatype);
+  if (!t) return MPIGX_ERR_TYPE;
+  int o;
+  if (op == MPIGX_REPLACE) o = O_REPLACE;
+  else if (op == MPIGX_NO_OP) o = O_NOOP;
+  else {
+    const int rc = validate(datatype, op, &t, &o);
+    if (rc) return rc;
+  }
+  *rep = t->rep;
+  *esize = t->size;
+  *oc = o;
+  return MPIGX_SUCCESS;
+}
+void progress_all(mpigx_comm* c) {
+  if (c->in_progress) return;
+  c->in_progress = true;
+  if (c->p2p) p2p_progress(c);
+  if (c->rma) rma_progress(c);
+  c->in_progress = false;
 }
 double wall() { return now_s(); }
 }  // namespace rt
@@ -819,6 +861,7 @@ int mpigx_comm_free(mpigx_comm_t c) {
     c->blocking = b;
   }
   (void)hipStreamSynchronize(c->stream);
+  rt::rma_destroy(c);
   rt::p2p_destroy(c);
   for (int q = 0; q < c->n; ++q) {
     if (!c->peer_opened[q]) continue;
@@ -833,6 +876,56 @@ int mpigx_comm_free(mpigx_comm_t c) {
   (void)hipHostFree(c->err);
   delete c;
   return rc;
+}
+
+// MPI_Comm_split (comm.jl:92-105): (color, key) are agreed over the host
+// control plane; the lowest (key, rank) member of each color creates the
+// group's unique id, a second exchange hands it out, then every member joins
+// its group with mpigx_comm_init_rank (groups rendezvous independently).
+int mpigx_comm_split(mpigx_comm_t c, int color, int key, mpigx_comm_t* out) {
+  int rc = check_comm(c);
+  if (rc) return rc;
+  if (!out) return MPIGX_ERR_ARG;
+  if (color < 0 && color != MPIGX_UNDEFINED) return MPIGX_ERR_ARG;
+  const int n = c->n;
+  int mine[2] = {color, key}, all[kMaxRanks][2];
+  rc = host_allgather(c, mine, sizeof mine, all);
+  if (rc) return rc;
+  int members[kMaxRanks], m = 0;
+  for (int q = 0; q < n; ++q)
+    if (color != MPIGX_UNDEFINED && all[q][0] == color) members[m++] = q;
+  // MPI order: by key, ties by rank in the parent
+  for (int i = 1; i < m; ++i)
+    for (int j = i; j > 0 && (all[members[j]][1] < all[members[j - 1]][1]); --j) {
+      const int t = members[j];
+      members[j] = members[j - 1];
+      members[j - 1] = t;
+    }
+  int sub = -1;
+  for (int i = 0; i < m; ++i)
+    if (members[i] == c->rank) sub = i;
+  mpigx_unique_id_t id;
+  memset(&id, 0, sizeof id);
+  if (sub == 0) {
+    rc = mpigx_get_unique_id(&id);
+    if (rc) return rc;
+  }
+  static_assert(sizeof(mpigx_unique_id_t) <= 256, "control-plane blob");
+  std::vector<mpigx_unique_id_t> ids(n);
+  rc = host_allgather(c, &id, sizeof id, ids.data());
+  if (rc) return rc;
+  if (sub < 0) {
+    *out = nullptr;
+    return MPIGX_SUCCESS;
+  }
+  mpigx_comm_t nc = nullptr;
+  rc = mpigx_comm_init_rank(&nc, m, &ids[members[0]], sub, c->device);
+  if (rc) return rc;
+  nc->stream = c->stream;
+  nc->blocking = c->blocking;
+  nc->order = c->order;
+  *out = nc;
+  return MPIGX_SUCCESS;
 }
 
 int mpigx_comm_rank(mpigx_comm_t c, int* rank) {

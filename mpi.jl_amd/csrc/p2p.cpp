@@ -367,6 +367,7 @@ bool complete(Req* r) {
 }
 
 void progress(mpigx_comm* c) {
+  if (c->rma && !c->in_progress) rt::rma_progress(c);  // waits here serve RMA targets too
   if (!c->p2p) return;
   post_sends(c);
   drain(c);

@@ -52,6 +52,45 @@ struct P2PMailbox {
   P2PEnvelope slot[kP2PSlots];
 };
 
+// One-sided (RMA) windows (rma.cpp).  Envelopes travel origin -> target in
+// the [origin][target] box of the window's slot; the TARGET applies Put /
+// Accumulate to its own memory (pulling the origin's buffer over xGMI) and
+// stores done = seq + 1.  Lock words are per target rank: 0 free, > 0 shared
+// holders, -1 exclusive.  Dynamic windows publish attached regions in
+// dyn[rank][*] (gen odd while being written).
+constexpr int kMaxWins = 16;
+constexpr int kRmaSlots = 16;
+constexpr int kMaxAttach = 16;
+struct alignas(64) RmaEnvelope {
+  std::atomic<uint64_t> posted;
+  std::atomic<uint64_t> done;
+  int kind;     // RmaKind (rma.cpp)
+  int op;       // OpCode / O_REPLACE / O_NOOP
+  int rep;      // element representation
+  int err;      // target-side result (MPI error class), valid once done
+  long long tdisp;  // byte offset into the target window (dynamic: absolute address)
+  long long count;  // elements (bytes for PUT)
+  long long res_off;  // GACC: byte offset of the old values in the target's scratch
+  unsigned long long buf_id;  // origin allocation (HIP buffer id), offset and handle
+  long long off;
+  unsigned long long raw;     // origin pointer (same-process origin)
+  hipIpcMemHandle_t h;
+};
+struct RmaBox {
+  RmaEnvelope slot[kRmaSlots];
+};
+struct DynRegion {
+  std::atomic<uint64_t> gen;
+  unsigned long long addr, size, buf_id;
+  long long off;
+  hipIpcMemHandle_t h;
+};
+struct WinShm {
+  std::atomic<int> lock[kMaxRanks];
+  RmaBox box[kMaxRanks][kMaxRanks];  // [origin][target]
+  DynRegion dyn[kMaxRanks][kMaxAttach];
+};
+
 struct ShmBlock {
   std::atomic<uint64_t> magic;
   int nranks;
@@ -60,9 +99,11 @@ struct ShmBlock {
   std::atomic<int> failed;
   ShmRank ranks[kMaxRanks];
   P2PMailbox box[kMaxRanks][kMaxRanks];  // [sender][receiver]
+  WinShm win[kMaxWins];
 };
 
 struct P2PState;  // p2p.cpp
+struct RmaState;  // rma.cpp
 
 }  // namespace mpigx
 
@@ -104,6 +145,7 @@ struct mpigx_comm {
     unsigned long long id;
     char* base;
     unsigned long long tick;
+    int pins;  // RMA windows holding this mapping (never evicted while > 0)
   };
   std::vector<LocalReg> lreg;
   std::vector<Import> imports;
@@ -117,6 +159,9 @@ struct mpigx_comm {
   mpigx::ShmBlock* shm = nullptr;
   // point-to-point engine (created on first use)
   mpigx::P2PState* p2p = nullptr;
+  // one-sided engine (created by the first window)
+  mpigx::RmaState* rma = nullptr;
+  bool in_progress = false;  // re-entrancy guard of rt::progress_all
   // tuning
   int max_blocks = 256;
   long long oneshot_max = 256 << 10;
@@ -131,10 +176,22 @@ int comm_check(mpigx_comm* c);
 int dtype_size(int datatype);  // bytes, or -1 if not a valid datatype handle
 bool export_buf(mpigx_comm* c, const void* p, unsigned long long* id, long long* off, hipIpcMemHandle_t* h);
 char* import_buf(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h);
+// as import_buf, and pin (+1) / unpin (-1) the mapping for a window's lifetime
+char* import_pinned(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h);
+void unpin(mpigx_comm* c, char* base);
+int host_allgather(mpigx_comm* c, const void* mine, int len, void* out);
+// every engine's progress (p2p + RMA target side); safe to call anywhere
+void progress_all(mpigx_comm* c);
+// RMA accumulate (datatype, op) check incl. REPLACE / NO_OP: rep, size, op code
+int acc_check(int datatype, int op, int* rep, int* esize, int* oc);
 double wall();
 // p2p.cpp
 void p2p_progress(mpigx_comm* c);
 void p2p_sync(mpigx_comm* c);     // drain the transfer stream
 void p2p_destroy(mpigx_comm* c);
+// rma.cpp
+void rma_progress(mpigx_comm* c);
+void rma_destroy(mpigx_comm* c);
+void rma_sync(mpigx_comm* c);  // drain the RMA stream
 }  // namespace rt
 }  // namespace mpigx

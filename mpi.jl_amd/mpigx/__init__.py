@@ -9,8 +9,17 @@ from . import consts
 from ._lib import HEADER_PATH, LIB_PATH, lib
 from .api import *  # noqa: F401,F403
 from .p2p import *  # noqa: F401,F403
+from .rma import *  # noqa: F401,F403
 from .api import (COMM_WORLD, IN_PLACE, Barrier, Buffer, Comm, Datatype, MPIError, Op, error_string,
                   reduce_local_multi)
+
+
+def free(obj):
+    """MPI.free: communicators (comm.jl) and windows (onesided.jl:85-92)."""
+    from . import api, rma
+    if isinstance(obj, rma.Win):
+        return rma.win_free(obj)
+    return api.free(obj)
 
 
 def __getattr__(name):

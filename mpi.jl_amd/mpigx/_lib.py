@@ -34,6 +34,7 @@ PROTOTYPES = {
     "mpigx_get_unique_id": (c_int, [ctypes.POINTER(UniqueId)]),
     "mpigx_comm_init_rank": (c_int, [ctypes.POINTER(c_void_p), c_int, ctypes.POINTER(UniqueId), c_int, c_int]),
     "mpigx_comm_free": (c_int, [c_void_p]),
+    "mpigx_comm_split": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_void_p)]),
     "mpigx_comm_rank": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
     "mpigx_comm_size": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
     "mpigx_comm_device": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
@@ -80,6 +81,26 @@ PROTOTYPES = {
     "mpigx_testsome": (c_int, [c_int, _IP, _IP, _IP, c_void_p]),
     "mpigx_cancel": (c_int, [_IP]),
     "mpigx_request_free": (c_int, [_IP]),
+    # one-sided
+    "mpigx_win_create": (c_int, [c_void_p, c_longlong, c_int, c_void_p, ctypes.POINTER(c_void_p)]),
+    "mpigx_win_create_dynamic": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
+    "mpigx_win_allocate_shared": (c_int, [c_longlong, c_int, c_void_p, c_void_p, ctypes.POINTER(c_void_p)]),
+    "mpigx_win_shared_query": (c_int, [c_void_p, c_int, ctypes.POINTER(c_longlong), _IP, c_void_p]),
+    "mpigx_win_free": (c_int, [ctypes.POINTER(c_void_p)]),
+    "mpigx_win_attach": (c_int, [c_void_p, c_void_p, c_longlong]),
+    "mpigx_win_detach": (c_int, [c_void_p, c_void_p]),
+    "mpigx_win_fence": (c_int, [c_int, c_void_p]),
+    "mpigx_win_flush": (c_int, [c_int, c_void_p]),
+    "mpigx_win_sync": (c_int, [c_void_p]),
+    "mpigx_win_lock": (c_int, [c_int, c_int, c_int, c_void_p]),
+    "mpigx_win_unlock": (c_int, [c_int, c_void_p]),
+    "mpigx_win_get_flavor": (c_int, [c_void_p, _IP]),
+    "mpigx_get": (c_int, [c_void_p, c_int, c_int, c_int, c_longlong, c_int, c_int, c_void_p]),
+    "mpigx_put": (c_int, [c_void_p, c_int, c_int, c_int, c_longlong, c_int, c_int, c_void_p]),
+    "mpigx_fetch_and_op": (c_int, [c_void_p, c_void_p, c_int, c_int, c_longlong, c_int, c_void_p]),
+    "mpigx_accumulate": (c_int, [c_void_p, c_int, c_int, c_int, c_longlong, c_int, c_int, c_int, c_void_p]),
+    "mpigx_get_accumulate": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_longlong, c_int, c_int,
+                                     c_int, c_void_p]),
     "mpigx_malloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),
     "mpigx_free": (c_int, [c_void_p]),
     "mpigx_memcpy": (c_int, [c_void_p, c_void_p, c_size_t]),

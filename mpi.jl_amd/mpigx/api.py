@@ -462,6 +462,35 @@ def Comm_dup(comm: Comm) -> Comm:
     return Comm(h, comm._rank, comm._size, comm.device, comm.host)
 
 
+def Comm_split(comm: Comm, color, key) -> Comm:
+    """comm.jl:92-105: color None (`nothing`) = MPI_UNDEFINED -> COMM_NULL (None)."""
+    col = C.MPI_UNDEFINED if color is None else int(color)
+    host = None
+    if comm.host is not None:
+        hc = ctypes.c_int(0)
+        _check(hostmpi.lib().MPI_Comm_split(comm.host, col, int(key), ctypes.byref(hc)))
+        host = hc.value if hc.value != C.MPI_COMM_NULL else None
+    h = None
+    rank = size = None
+    if comm.val:
+        hv = ctypes.c_void_p()
+        _check(lib().mpigx_comm_split(comm.val, col, int(key), ctypes.byref(hv)))
+        if hv.value:
+            h = hv
+            r, s = ctypes.c_int(), ctypes.c_int()
+            lib().mpigx_comm_rank(h, ctypes.byref(r))
+            lib().mpigx_comm_size(h, ctypes.byref(s))
+            rank, size = r.value, s.value
+    if host is not None and rank is None:
+        r, s = ctypes.c_int(), ctypes.c_int()
+        hostmpi.lib().MPI_Comm_rank(host, ctypes.byref(r))
+        hostmpi.lib().MPI_Comm_size(host, ctypes.byref(s))
+        rank, size = r.value, s.value
+    if h is None and host is None:
+        return None
+    return Comm(h, rank, size, comm.device, host)
+
+
 def Comm_split_type(comm: Comm, split_type, key, info=None) -> Comm:
     """comm.jl:107: COMM_TYPE_SHARED on one node is every rank."""
     if split_type != C.MPI_COMM_TYPE_SHARED:
