@@ -130,6 +130,7 @@ struct VArgs {
 constexpr int kMaxXfer = 16;
 struct XferArgs {
   int nseg;
+  int coherent;  // system-scope acquire at start / release at end (pull_fences())
   int blk0[kMaxXfer + 1];       // first block of each segment (prefix sums)
   char* dst[kMaxXfer];
   const char* src[kMaxXfer];
@@ -145,6 +146,7 @@ struct AccArgs {
   void* dst;
   void* res;  // may be null
   long long count;
+  int coherent;  // system-scope acquire at start / release at end (pull_fences())
 };
 
 struct ScanArgs {

@@ -172,6 +172,7 @@ hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a) {
 // [blk0[j], blk0[j+1]) and is cut into equal 16-B-multiple slices.  The
 // receiver pulls from the sender's (IPC-mapped) buffer, so writes stay local.
 __global__ __launch_bounds__(kThreads) void xfer_kernel(XferArgs A) {
+  pull_acquire(A.coherent);
   const int b = blockIdx.x;
   int j = 0;
   while (j + 1 < A.nseg && b >= A.blk0[j + 1]) ++j;
@@ -179,6 +180,7 @@ __global__ __launch_bounds__(kThreads) void xfer_kernel(XferArgs A) {
   const long long slice = ((A.bytes[j] + g - 1) / g + 15) & ~15ll;
   const long long lo = lmin(k * slice, A.bytes[j]), hi = lmin(lo + slice, A.bytes[j]);
   block_copy(A.dst[j] + lo, A.src[j] + lo, hi - lo);
+  pull_release(A.coherent);
 }
 
 hipError_t launch_xfer(hipStream_t s, const XferArgs& a) {

@@ -399,6 +399,30 @@ __device__ __forceinline__ void block_gather(char* const (&dst)[NMAX], const cha
 }
 
 // ---------------------------------------------------------------------------
+// Pull kernels launched after a HOST-side hand-off (p2p / RMA: the producer's
+// kernel finished and the host saw it) read peer memory mapped through IPC.
+// Kernel boundaries order local memory, but this CU's L1 / this XCD's L2 may
+// still hold lines of the peer allocation from an earlier pull of the same
+// bytes, so every block drops them first (system-scope acquire, one lane,
+// then the block barrier) and publishes its own stores at system scope at
+// the end (a peer may pull them next).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void pull_acquire(int on) {
+  if (!on) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void pull_release(int on) {
+  if (!on) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+// ---------------------------------------------------------------------------
 // cross-rank barrier of block `blockIdx.x` on every rank, at epoch `ep`.
 // Producer side: every wave drains its stores, block barrier, one wave issues
 // a SYSTEM-scope release (writes this XCD's L2 back so peers reading our HBM

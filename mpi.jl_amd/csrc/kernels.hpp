@@ -289,6 +289,7 @@ __global__ __launch_bounds__(kThreads) void acc_kernel(AccArgs A) {
   const T* __restrict__ src = reinterpret_cast<const T*>(A.src);
   T* __restrict__ dst = reinterpret_cast<T*>(A.dst);
   T* __restrict__ res = reinterpret_cast<T*>(A.res);
+  pull_acquire(A.coherent);
   const long long n = A.count, nt = (long long)gridDim.x * blockDim.x;
   constexpr int U = 4;  // independent elements in flight per thread
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(kThreads) void acc_kernel(AccArgs A) {
     if constexpr (OP::code == O_REPLACE) dst[i] = src[i];
     else if constexpr (OP::code != O_NOOP) dst[i] = OP::apply(t, src[i]);
   }
+  pull_release(A.coherent);
 }
 
 }  // namespace mpigx

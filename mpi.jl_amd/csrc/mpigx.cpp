@@ -353,8 +353,10 @@ bool zc_export(mpigx_comm* c, const void* p, unsigned long long* id, long long* 
 }
 
 char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h) {
+  // keyed by the handle too: the HIP runtime may hand a recycled buffer id to
+  // a new allocation (seen with free/alloc of equal sizes), whose handle differs
   for (auto& im : c->imports)
-    if (im.peer == peer && im.id == id) {
+    if (im.peer == peer && im.id == id && !memcmp(&im.h, &h, sizeof h)) {
       im.tick = ++c->tick;
       return im.base;
     }
@@ -376,7 +378,7 @@ char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemH
       c->imports.erase(c->imports.begin() + oldest);
     }
   }
-  c->imports.push_back({peer, id, (char*)ptr, ++c->tick, 0});
+  c->imports.push_back({peer, id, (char*)ptr, ++c->tick, 0, h});
   return (char*)ptr;
 }
 
@@ -661,6 +663,10 @@ void progress_all(mpigx_comm* c) {
   c->in_progress = false;
 }
 double wall() { return now_s(); }
+int pull_fences() {
+  static const int v = (int)env_ll("MPIGX_PULL_FENCES", 1);
+  return v;
+}
 }  // namespace rt
 }  // namespace mpigx
 

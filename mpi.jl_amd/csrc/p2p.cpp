@@ -252,6 +252,7 @@ void flush(mpigx_comm* c) {
     XferArgs a;
     memset(&a, 0, sizeof a);
     a.nseg = (int)m;
+    a.coherent = rt::pull_fences();
     bool ok = true;
     for (size_t j = 0; j < m; ++j) {
       Req* r = P->batch[i + j];

@@ -85,7 +85,7 @@ struct mpigx_win {
   char* peer_base[kMaxRanks] = {};
   long long peer_size[kMaxRanks] = {};
   int peer_du[kMaxRanks] = {};
-  // Get_accumulate scratch: slot_bytes per origin
+  // Get_accumulate scratch (the communicator's, RmaState): slot_bytes per origin
   char* scratch = nullptr;
   long long slot_bytes = 0;
   char* peer_scratch[kMaxRanks] = {};
@@ -111,6 +111,13 @@ struct RmaState {
   unsigned used = 0;  // window slots in use (identical on every rank)
   std::vector<mpigx_win*> wins;
   WinShm* local = nullptr;  // single-rank communicator (no shm block)
+  // Get_accumulate / Fetch_and_op old values: one slot per origin, allocated
+  // and exchanged once (with the first window) and shared by all windows —
+  // an origin has at most one such operation in flight (acc_common waits).
+  char* scratch = nullptr;
+  long long slot_bytes = 0;
+  char* peer_scratch[kMaxRanks] = {};
+  std::vector<char*> pinned;
 };
 }  // namespace mpigx
 
@@ -189,6 +196,7 @@ int apply_one(mpigx_win* w, int o, RmaEnvelope* e, hipStream_t ws) {
     XferArgs a;
     memset(&a, 0, sizeof a);
     a.nseg = 1;
+    a.coherent = rt::pull_fences();
     long long g = (bytes + (64 << 10) - 1) / (64 << 10);
     a.blk0[1] = (int)std::max(1ll, std::min(g, 256ll));
     a.dst[0] = dst;
@@ -201,6 +209,7 @@ int apply_one(mpigx_win* w, int o, RmaEnvelope* e, hipStream_t ws) {
   a.dst = dst;
   a.res = nullptr;
   a.count = e->count;
+  a.coherent = rt::pull_fences();
   if (e->kind == RK_GACC) {
     if (e->res_off < 0 || e->res_off + bytes > w->slot_bytes * c->n) return MPIGX_ERR_INTERN;
     a.res = w->scratch + e->res_off;
@@ -388,6 +397,7 @@ int pull(mpigx_win* w, void* dst, const char* src, long long bytes) {
   XferArgs a;
   memset(&a, 0, sizeof a);
   a.nseg = 1;
+  a.coherent = rt::pull_fences();
   long long g = (bytes + (64 << 10) - 1) / (64 << 10);
   a.blk0[1] = (int)std::max(1ll, std::min(g, 256ll));
   a.dst[0] = (char*)dst;
@@ -439,7 +449,6 @@ static_assert(sizeof(WinBlob) <= 256, "control-plane blob");
 int free_local(mpigx_win* w) {
   mpigx_comm* c = w->c;
   for (char* p : w->pinned) rt::unpin(c, p);
-  if (w->scratch) (void)hipFree(w->scratch);
   if (w->shared_alloc) (void)hipFree(w->shared_alloc);
   if (c->rma) {
     c->rma->used &= ~(1u << w->slot);
@@ -488,24 +497,25 @@ int win_setup(mpigx_comm* c, int flavor, char* base, long long size, int disp_un
   std::atomic_thread_fence(std::memory_order_seq_cst);
 
   const int n = c->n;
-  long long sb = env_ll("MPIGX_RMA_SCRATCH", 4ll << 20);
-  w->slot_bytes = std::max(256ll, (sb / n) & ~255ll);
+  const bool first = R->scratch == nullptr;  // identical on every rank (windows are collective)
   WinBlob mine;
   memset(&mine, 0, sizeof mine);
   mine.ok = 1;
   mine.du = disp_unit;
   mine.size = flavor == MPIGX_WIN_FLAVOR_DYNAMIC ? 0 : size;
   mine.raw = (unsigned long long)(uintptr_t)base;
-  if (hipMalloc(&w->scratch, w->slot_bytes * n) != hipSuccess) {
-    (void)hipGetLastError();
-    w->scratch = nullptr;
-    mine.ok = 0;
+  if (first) {
+    const long long sb = env_ll("MPIGX_RMA_SCRATCH", 4ll << 20);
+    R->slot_bytes = std::max(256ll, (sb / n) & ~255ll);
+    if (hipMalloc(&R->scratch, R->slot_bytes * n) != hipSuccess) {
+      (void)hipGetLastError();
+      R->scratch = nullptr;
+      mine.ok = 0;
+    }
+    mine.sraw = (unsigned long long)(uintptr_t)R->scratch;
+    if (n > 1 && mine.ok && !rt::export_buf(c, R->scratch, &mine.sid, &mine.soff, &mine.sh)) mine.ok = 0;
   }
-  mine.sraw = (unsigned long long)(uintptr_t)w->scratch;
-  if (n > 1 && mine.ok) {
-    if (mine.size > 0 && !rt::export_buf(c, base, &mine.id, &mine.off, &mine.h)) mine.ok = 0;
-    if (!rt::export_buf(c, w->scratch, &mine.sid, &mine.soff, &mine.sh)) mine.ok = 0;
-  }
+  if (n > 1 && mine.ok && mine.size > 0 && !rt::export_buf(c, base, &mine.id, &mine.off, &mine.h)) mine.ok = 0;
   WinBlob all[kMaxRanks];
   rc = rt::host_allgather(c, &mine, sizeof mine, all);
   if (rc) {
@@ -520,7 +530,7 @@ int win_setup(mpigx_comm* c, int flavor, char* base, long long size, int disp_un
     w->peer_size[q] = all[q].size;
     if (same_process(c, q)) {
       w->peer_base[q] = (char*)(uintptr_t)all[q].raw;
-      w->peer_scratch[q] = (char*)(uintptr_t)all[q].sraw;
+      if (first) R->peer_scratch[q] = (char*)(uintptr_t)all[q].sraw;
       continue;
     }
     if (all[q].size > 0) {
@@ -532,14 +542,19 @@ int win_setup(mpigx_comm* c, int flavor, char* base, long long size, int disp_un
       w->pinned.push_back(b);
       w->peer_base[q] = b + all[q].off;
     }
-    char* s = rt::import_pinned(c, q, all[q].sid, all[q].sh);
-    if (!s) {
-      ok = 0;
-      break;
+    if (first) {
+      char* s = rt::import_pinned(c, q, all[q].sid, all[q].sh);
+      if (!s) {
+        ok = 0;
+        break;
+      }
+      R->pinned.push_back(s);
+      R->peer_scratch[q] = s + all[q].soff;
     }
-    w->pinned.push_back(s);
-    w->peer_scratch[q] = s + all[q].soff;
   }
+  w->scratch = R->scratch;
+  w->slot_bytes = R->slot_bytes;
+  for (int q = 0; q < n; ++q) w->peer_scratch[q] = R->peer_scratch[q];
   int oks[kMaxRanks];
   rc = rt::host_allgather(c, &ok, sizeof ok, oks);
   if (!rc)
@@ -584,6 +599,8 @@ void rma_destroy(mpigx_comm* c) {
   if (!R) return;
   (void)hipStreamSynchronize(R->ws);
   while (!R->wins.empty()) free_local(R->wins.back());
+  for (char* p : R->pinned) rt::unpin(c, p);
+  if (R->scratch) (void)hipFree(R->scratch);
   (void)hipEventDestroy(R->ev);
   (void)hipStreamDestroy(R->ws);
   free(R->local);

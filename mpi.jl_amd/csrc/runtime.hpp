@@ -146,6 +146,7 @@ struct mpigx_comm {
     char* base;
     unsigned long long tick;
     int pins;  // RMA windows holding this mapping (never evicted while > 0)
+    hipIpcMemHandle_t h;
   };
   std::vector<LocalReg> lreg;
   std::vector<Import> imports;
@@ -185,6 +186,7 @@ void progress_all(mpigx_comm* c);
 // RMA accumulate (datatype, op) check incl. REPLACE / NO_OP: rep, size, op code
 int acc_check(int datatype, int op, int* rep, int* esize, int* oc);
 double wall();
+int pull_fences();  // MPIGX_PULL_FENCES (default 1): coherent flag of p2p / RMA pull kernels
 // p2p.cpp
 void p2p_progress(mpigx_comm* c);
 void p2p_sync(mpigx_comm* c);     // drain the transfer stream

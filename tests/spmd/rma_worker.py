@@ -299,6 +299,7 @@ def multi_origin():
     MPI.Get(got, 0, win)
     MPI.Win_unlock(0, win)
     rec("shared_lock_get", got=bits(got))
+    MPI.Barrier(comm)  # every Get of the shared epoch is complete before anyone accumulates
     # passive-target accumulates from everyone, then a fence
     o4 = A(np.full(6, rank + 1))
     MPI.Win_lock(MPI.LOCK_SHARED, 0, 0, win)
