@@ -349,6 +349,40 @@ int mpigx_get_accumulate(const void *origin_addr, int origin_count, int origin_d
                          long long target_disp, int target_count, int target_datatype, int op,
                          mpigx_win_t win);
 
+/* ---- derived datatypes (src/datatypes.jl:62-318) ---
+ * The MPI_Type_* constructors MPI.Types ccalls, for device buffers: handles
+ * are `int`s in MPICH's derived-type space (0x8c000000 | index), usable
+ * wherever a datatype is taken once committed — point-to-point (strided and
+ * dense SubArrays, buffers.jl:104-117; padded isbits structs,
+ * datatypes.jl:269-316) and the byte-moving collectives (Bcast, Allgather,
+ * Alltoall, Gather, Scatter), which pack non-contiguous types on device
+ * (pack_kernel) around the contiguous algorithm.  Reductions accept derived
+ * types that are contiguous runs of one predefined type.  lb / extent /
+ * sizes follow MPICH 3.3.2 (tests/golden/types_golden.json). */
+#define MPIGX_ORDER_C 56
+#define MPIGX_ORDER_FORTRAN 57
+#define MPIGX_DATATYPE_NULL 0x0c000000
+int mpigx_type_contiguous(int count, int oldtype, int *newtype);
+int mpigx_type_vector(int count, int blocklength, int stride, int oldtype, int *newtype);
+int mpigx_type_create_hvector(int count, int blocklength, long long stride, int oldtype, int *newtype);
+int mpigx_type_create_subarray(int ndims, const int *sizes, const int *subsizes, const int *starts, int order,
+                               int oldtype, int *newtype);
+int mpigx_type_create_struct(int count, const int *blocklengths, const long long *displacements,
+                             const int *types, int *newtype);
+int mpigx_type_create_resized(int oldtype, long long lb, long long extent, int *newtype);
+int mpigx_type_commit(int *datatype);
+int mpigx_type_free(int *datatype);
+int mpigx_type_get_extent(int datatype, long long *lb, long long *extent);
+int mpigx_type_get_true_extent(int datatype, long long *true_lb, long long *true_extent);
+int mpigx_type_size_x(int datatype, long long *size);
+/* MPI_Pack / MPI_Unpack / MPI_Pack_size on device buffers (stream: hipStream_t
+ * or NULL; blocking).  Pack layout = MPI's (typemap order, no padding). */
+int mpigx_pack_size(int incount, int datatype, long long *size);
+int mpigx_pack(const void *inbuf, int incount, int datatype, void *outbuf, long long outsize,
+               long long *position, void *stream);
+int mpigx_unpack(const void *inbuf, long long insize, long long *position, void *outbuf, int outcount,
+                 int datatype, void *stream);
+
 /* ---- device buffers (north-star subsystem 1: the ROCBuffer backing) ----- */
 int mpigx_malloc(void **ptr, size_t bytes);
 int mpigx_free(void *ptr);

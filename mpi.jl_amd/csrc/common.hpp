@@ -149,6 +149,24 @@ struct AccArgs {
   int coherent;  // system-scope acquire at start / release at end (pull_fences())
 };
 
+// Derived datatypes (types.cpp): n blocks of len bytes at off + i*stride.
+struct TypeRun {
+  long long off, len, n, stride;
+};
+// Pack (typed -> contiguous) or unpack (contiguous -> typed) `units` W-byte
+// units of a packed stream of instances of one type (extent apart).
+struct PackArgs {
+  char* typed;
+  char* contig;
+  const TypeRun* runs;   // device copy, typemap order
+  const long long* pfx;  // packed bytes before run r within one instance (nruns + 1)
+  int nruns;
+  int w;
+  int unpack;
+  int coherent;
+  long long size, extent, units;
+};
+
 struct ScanArgs {
   PeerView pv;
   int exclusive;

@@ -188,6 +188,52 @@ hipError_t launch_xfer(hipStream_t s, const XferArgs& a) {
   return hipGetLastError();
 }
 
+// Derived-datatype pack / unpack (types.cpp): unit u = packed bytes
+// [u*W, u*W+W) of the stream -> instance, run (binary search over the
+// per-instance prefix), block, byte -> typed address.  Gather/scatter
+// bound by HBM (or xGMI when `contig` is a peer's buffer).
+template <int W>
+__global__ __launch_bounds__(kThreads) void pack_kernel(PackArgs A) {
+  pull_acquire(A.coherent);
+  using V = typename std::conditional<W == 16, u32x4,
+            typename std::conditional<W == 8, uint64_t,
+            typename std::conditional<W == 4, uint32_t,
+            typename std::conditional<W == 2, uint16_t, uint8_t>::type>::type>::type>::type;
+  const long long nt = (long long)gridDim.x * blockDim.x;
+  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < A.units; u += nt) {
+    const long long p = u * W;
+    const long long k = p / A.size, r = p - k * A.size;
+    int lo = 0;
+    if (A.nruns > 1) {
+      int hi = A.nruns - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (A.pfx[mid] <= r) lo = mid;
+        else hi = mid - 1;
+      }
+    }
+    const TypeRun R = A.runs[lo];
+    const long long q = r - A.pfx[lo], i = q / R.len, b = q - i * R.len;
+    const long long t = k * A.extent + R.off + i * R.stride + b;
+    if (A.unpack) *reinterpret_cast<V*>(A.typed + t) = *reinterpret_cast<const V*>(A.contig + p);
+    else *reinterpret_cast<V*>(A.contig + p) = *reinterpret_cast<const V*>(A.typed + t);
+  }
+  pull_release(A.coherent);
+}
+
+hipError_t launch_pack(hipStream_t s, const PackArgs& a) {
+  long long g = (a.units + kThreads - 1) / kThreads;
+  g = g < 1 ? 1 : (g > 4096 ? 4096 : g);
+  switch (a.w) {
+    case 16: hipLaunchKernelGGL(pack_kernel<16>, dim3((unsigned)g), dim3(kThreads), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(pack_kernel<8>, dim3((unsigned)g), dim3(kThreads), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(pack_kernel<4>, dim3((unsigned)g), dim3(kThreads), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(pack_kernel<2>, dim3((unsigned)g), dim3(kThreads), 0, s, a); break;
+    default: hipLaunchKernelGGL(pack_kernel<1>, dim3((unsigned)g), dim3(kThreads), 0, s, a); break;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a) {
   if (a.pv.n <= 8)
     hipLaunchKernelGGL(copy_kernel<8>, grid, dim3(kThreads), 0, s, a);

@@ -25,5 +25,6 @@ MPIGX_DECL_REP(bf16)
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a);
 hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a);
 hipError_t launch_xfer(hipStream_t s, const XferArgs& a);
+hipError_t launch_pack(hipStream_t s, const PackArgs& a);
 
 }  // namespace mpigx

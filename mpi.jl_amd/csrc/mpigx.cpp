@@ -516,6 +516,37 @@ int check_comm(mpigx_comm* c) {
   return MPIGX_SUCCESS;
 }
 
+// Pooled device temporaries for derived-type packing in collectives (used on
+// the comm's stream only, so stream order makes reuse safe).
+char* tmp_get(mpigx_comm* c, long long bytes) {
+  size_t best = c->tmp_free.size();
+  for (size_t i = 0; i < c->tmp_free.size(); ++i)
+    if (c->tmp_free[i].first >= bytes && (best == c->tmp_free.size() || c->tmp_free[i].first < c->tmp_free[best].first))
+      best = i;
+  if (best < c->tmp_free.size()) {
+    char* p = c->tmp_free[best].second;
+    c->tmp_used.push_back(c->tmp_free[best]);
+    c->tmp_free.erase(c->tmp_free.begin() + best);
+    return p;
+  }
+  const long long cap = (bytes + (1 << 20) - 1) & ~((1ll << 20) - 1);
+  char* p = nullptr;
+  if (hipMalloc(&p, cap) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  c->tmp_used.push_back({cap, p});
+  return p;
+}
+void tmp_put(mpigx_comm* c, char* p, long long) {
+  for (size_t i = 0; i < c->tmp_used.size(); ++i)
+    if (c->tmp_used[i].second == p) {
+      c->tmp_free.push_back(c->tmp_used[i]);
+      c->tmp_used.erase(c->tmp_used.begin() + i);
+      return;
+    }
+}
+
 int copy_n1(mpigx_comm* c, void* dst, const void* src, size_t bytes) {
   if (dst != src && bytes) HIPCK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
   return finish(c);
@@ -709,7 +740,13 @@ int mpigx_op_valid(int datatype, int op) { return validate(datatype, op, nullptr
 
 int mpigx_type_size(int datatype, int* size) {
   const TypeInfo* t = find_type(datatype);
-  if (!t) return MPIGX_ERR_TYPE;
+  if (!t) {
+    long long s = 0;
+    const int rc = mpigx_type_size_x(datatype, &s);
+    if (rc) return rc;
+    if (size) *size = s > 0x7fffffff ? MPIGX_UNDEFINED : (int)s;
+    return MPIGX_SUCCESS;
+  }
   if (size) *size = t->size;
   return MPIGX_SUCCESS;
 }
@@ -876,6 +913,8 @@ int mpigx_comm_free(mpigx_comm_t c) {
   }
   for (auto& im : c->imports) (void)hipIpcCloseMemHandle(im.base);
   if (c->shm) munmap(c->shm, sizeof(ShmBlock));
+  for (auto& b : c->tmp_free) (void)hipFree(b.second);
+  for (auto& b : c->tmp_used) (void)hipFree(b.second);
   (void)hipFree(c->stage);
   (void)hipFree(c->sig);
   (void)hipFree(c->dcount_dev);
@@ -1020,7 +1059,7 @@ int mpigx_comm_probe(mpigx_comm_t c, int kind, long long bytes, double* seconds)
   return finish(c);
 }
 
-int mpigx_bcast(void* buf, int count, int datatype, int root, mpigx_comm_t c) {
+static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t c) {
   int rc = check_comm(c);
   if (rc) return rc;
   const TypeInfo* t = find_type(datatype);
@@ -1100,23 +1139,120 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
   return finish(c);
 }
 
+// ---------------------------------------------------------------------------
+// Derived datatypes in the byte-moving collectives: a
+// contiguous derived type travels as bytes; any other one is packed on device
+// (types.cpp pack_kernel) into a pooled temporary on the comm's stream, moved
+// by the contiguous algorithm as MPI_BYTE, and unpacked on the same stream.
+// ---------------------------------------------------------------------------
+static bool derived(int h) { return rt::dtype_size(h) < 0; }
+
+static int bytes_of(int type, long long count, rt::TypeDesc* d, int* out) {
+  if (rt::type_info(type, d)) return MPIGX_ERR_TYPE;
+  if (count < 0) return MPIGX_ERR_COUNT;
+  const long long b = count * d->size;
+  if (b > 0x7fffffff) return MPIGX_ERR_COUNT;
+  *out = (int)b;
+  return MPIGX_SUCCESS;
+}
+
+static int pack_on(mpigx_comm* c, int type, const void* typed, long long count, char* tmp, long long bytes,
+                   int unpack) {
+  const int rc = rt::type_pack(type, typed, count, tmp, bytes, unpack, c->device, c->stream);
+  if (!rc) c->unflagged = true;  // the final finish() drains the stream
+  return rc;
+}
+
+int mpigx_bcast(void* buf, int count, int datatype, int root, mpigx_comm_t c) {
+  if (!derived(datatype)) return bcast_impl(buf, count, datatype, root, c);
+  int rc = check_comm(c);
+  if (rc) return rc;
+  rt::TypeDesc d;
+  int nb;
+  if ((rc = bytes_of(datatype, count, &d, &nb))) return rc;
+  if (d.contig) return bcast_impl(buf, nb, MPIGX_BYTE, root, c);
+  if (root < 0 || root >= c->n) return MPIGX_ERR_ROOT;
+  if (nb == 0) return MPIGX_SUCCESS;
+  char* tmp = tmp_get(c, nb);
+  if (!tmp) return MPIGX_ERR_NO_MEM;
+  if (c->rank == root) rc = pack_on(c, datatype, buf, count, tmp, nb, 0);
+  if (!rc) rc = bcast_impl(tmp, nb, MPIGX_BYTE, root, c);
+  if (!rc && c->rank != root) rc = pack_on(c, datatype, buf, count, tmp, nb, 1);
+  if (!rc) rc = finish(c);
+  tmp_put(c, tmp, nb);
+  return rc;
+}
+
+static int gather_like_any(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount,
+                           int recvtype, mpigx_comm_t c, bool alltoall) {
+  const bool inplace = sendbuf == MPIGX_IN_PLACE;
+  if (!derived(recvtype) && (inplace || !derived(sendtype)))
+    return gather_like(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, c, alltoall);
+  int rc = check_comm(c);
+  if (rc) return rc;
+  const int n = c->n, r = c->rank;
+  rt::TypeDesc rd, sd;
+  int rb, sb = 0;
+  if ((rc = bytes_of(recvtype, recvcount, &rd, &rb))) return rc;  // bytes per rank block
+  if (!inplace && (rc = bytes_of(sendtype, sendcount, &sd, &sb))) return rc;
+  if (!inplace && sb != rb) return MPIGX_ERR_ARG;
+  if (rb == 0) return MPIGX_SUCCESS;
+  const long long ninst = (long long)n * recvcount;  // recv elements in the whole buffer
+  // receive side: the typed buffer, or a packed temporary of n blocks
+  char* rtmp = nullptr;
+  char* rdst = (char*)recvbuf;
+  if (!rd.contig) {
+    if (!(rtmp = tmp_get(c, (long long)n * rb))) return MPIGX_ERR_NO_MEM;
+    rdst = rtmp;
+  }
+  const void* src = sendbuf;
+  char* stmp = nullptr;
+  if (inplace) {
+    if (rtmp) {  // my block(s) of the typed recvbuf -> the packed temporary
+      if (alltoall) rc = pack_on(c, recvtype, recvbuf, ninst, rtmp, (long long)n * rb, 0);
+      else rc = pack_on(c, recvtype, (const char*)recvbuf + (long long)r * recvcount * rd.extent, recvcount,
+                        rtmp + (long long)r * rb, rb, 0);
+    }
+  } else if (derived(sendtype) && !sd.contig) {
+    const long long sinst = alltoall ? (long long)n * sendcount : sendcount;
+    if (!(stmp = tmp_get(c, sinst * sd.size))) rc = MPIGX_ERR_NO_MEM;
+    else rc = pack_on(c, sendtype, sendbuf, sinst, stmp, sinst * sd.size, 0);
+    src = stmp;
+  }
+  if (!rc) rc = gather_like(src, rb, MPIGX_BYTE, rdst, rb, MPIGX_BYTE, c, alltoall);
+  if (!rc && rtmp) rc = pack_on(c, recvtype, recvbuf, ninst, rtmp, (long long)n * rb, 1);
+  if (!rc) rc = finish(c);
+  if (stmp) tmp_put(c, stmp, 0);
+  if (rtmp) tmp_put(c, rtmp, 0);
+  return rc;
+}
+
 int mpigx_allgather(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
                     mpigx_comm_t c) {
-  return gather_like(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, c, false);
+  return gather_like_any(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, c, false);
 }
 int mpigx_alltoall(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
                    mpigx_comm_t c) {
-  return gather_like(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, c, true);
+  return gather_like_any(sendbuf, sendcount, sendtype, recvbuf, recvcount, recvtype, c, true);
 }
 
 // ---------------------------------------------------------------------------
 // v-collectives and rooted variants (collective.jl:90-578)
 // ---------------------------------------------------------------------------
+// Element size for the v-collectives: predefined types and contiguous derived
+// types (displacements are in extents, equal to sizes only then).
+static int vsize(int dtype, int* out) {
+  rt::TypeDesc d;
+  if (rt::type_info(dtype, &d) || !d.contig || d.size > 0x7fffffff) return MPIGX_ERR_TYPE;
+  *out = (int)d.size;
+  return MPIGX_SUCCESS;
+}
+
 static int type_bytes(int dtype, long long count, long long* out) {
-  const TypeInfo* t = find_type(dtype);
-  if (!t) return MPIGX_ERR_TYPE;
+  int sz;
+  if (vsize(dtype, &sz)) return MPIGX_ERR_TYPE;
   if (count < 0) return MPIGX_ERR_COUNT;
-  *out = count * t->size;
+  *out = count * sz;
   return MPIGX_SUCCESS;
 }
 
@@ -1133,7 +1269,7 @@ static int gather_common(const void* send, int scount, int stype, void* recv, in
   VSpec s;
   int rsz = 0;
   if (isroot) {
-    if ((rc = mpigx_type_size(rtype, &rsz))) return rc;
+    if ((rc = vsize(rtype, &rsz))) return rc;
     if (!recv) return MPIGX_ERR_BUFFER;
     for (int p = 0; p < n; ++p) {
       const long long cnt = rcounts ? rcounts[p] : rcount;
@@ -1161,7 +1297,41 @@ static int gather_common(const void* send, int scount, int stype, void* recv, in
 
 int mpigx_gather(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
                  int root, mpigx_comm_t c) {
-  return gather_common(sendbuf, sendcount, sendtype, recvbuf, recvcount, nullptr, nullptr, recvtype, root, c);
+  const bool inplace = sendbuf == MPIGX_IN_PLACE;
+  int rc = check_comm(c);
+  if (rc) return rc;
+  if (root < 0 || root >= c->n) return MPIGX_ERR_ROOT;
+  const bool isroot = c->rank == root;
+  if ((inplace || !derived(sendtype)) && (!isroot || !derived(recvtype)))
+    return gather_common(sendbuf, sendcount, sendtype, recvbuf, recvcount, nullptr, nullptr, recvtype, root, c);
+  // derived types: pack my contribution / receive packed blocks at the root
+  rt::TypeDesc sd, rd;
+  int sb = 0, rb = 0;
+  if (!inplace && (rc = bytes_of(sendtype, sendcount, &sd, &sb))) return rc;
+  if (isroot && (rc = bytes_of(recvtype, recvcount, &rd, &rb))) return rc;
+  if (!isroot) rb = sb;
+  const int n = c->n;
+  char *stmp = nullptr, *rtmp = nullptr;
+  const void* src = sendbuf;
+  void* dst = recvbuf;
+  if (!inplace && !sd.contig) {
+    if (!(stmp = tmp_get(c, sb > 0 ? sb : 1))) return MPIGX_ERR_NO_MEM;
+    rc = pack_on(c, sendtype, sendbuf, sendcount, stmp, sb, 0);
+    src = stmp;
+  }
+  if (!rc && isroot && !rd.contig) {
+    if (!(rtmp = tmp_get(c, (long long)n * rb > 0 ? (long long)n * rb : 1))) rc = MPIGX_ERR_NO_MEM;
+    else if (inplace)
+      rc = pack_on(c, recvtype, (const char*)recvbuf + (long long)root * recvcount * rd.extent, recvcount,
+                   rtmp + (long long)root * rb, rb, 0);
+    dst = rtmp;
+  }
+  if (!rc) rc = gather_common(src, inplace ? 0 : sb, MPIGX_BYTE, dst, rb, nullptr, nullptr, MPIGX_BYTE, root, c);
+  if (!rc && rtmp) rc = pack_on(c, recvtype, recvbuf, (long long)n * recvcount, rtmp, (long long)n * rb, 1);
+  if (!rc) rc = finish(c);
+  if (stmp) tmp_put(c, stmp, 0);
+  if (rtmp) tmp_put(c, rtmp, 0);
+  return rc;
 }
 int mpigx_gatherv(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, const int* recvcounts,
                   const int* displs, int recvtype, int root, mpigx_comm_t c) {
@@ -1181,7 +1351,7 @@ static int scatter_common(const void* send, int scount, const int* scounts, cons
   VSpec s;
   if (isroot) {
     int ssz = 0;
-    if ((rc = mpigx_type_size(stype, &ssz))) return rc;
+    if ((rc = vsize(stype, &ssz))) return rc;
     if (!send) return MPIGX_ERR_BUFFER;
     s.ncopy = n;
     for (int q = 0; q < n; ++q) {
@@ -1208,7 +1378,37 @@ static int scatter_common(const void* send, int scount, const int* scounts, cons
 
 int mpigx_scatter(const void* sendbuf, int sendcount, int sendtype, void* recvbuf, int recvcount, int recvtype,
                   int root, mpigx_comm_t c) {
-  return scatter_common(sendbuf, sendcount, nullptr, nullptr, sendtype, recvbuf, recvcount, recvtype, root, c);
+  const bool inplace = recvbuf == MPIGX_IN_PLACE;
+  int rc = check_comm(c);
+  if (rc) return rc;
+  if (root < 0 || root >= c->n) return MPIGX_ERR_ROOT;
+  const bool isroot = c->rank == root;
+  if ((!isroot || !derived(sendtype)) && (inplace || !derived(recvtype)))
+    return scatter_common(sendbuf, sendcount, nullptr, nullptr, sendtype, recvbuf, recvcount, recvtype, root, c);
+  rt::TypeDesc sd, rd;
+  int sb = 0, rb = 0;
+  if (!inplace && (rc = bytes_of(recvtype, recvcount, &rd, &rb))) return rc;
+  if (isroot && (rc = bytes_of(sendtype, sendcount, &sd, &sb))) return rc;
+  if (!isroot) sb = rb;
+  const int n = c->n;
+  char *stmp = nullptr, *rtmp = nullptr;
+  const void* src = sendbuf;
+  void* dst = recvbuf;
+  if (isroot && !sd.contig) {
+    if (!(stmp = tmp_get(c, (long long)n * sb > 0 ? (long long)n * sb : 1))) return MPIGX_ERR_NO_MEM;
+    rc = pack_on(c, sendtype, sendbuf, (long long)n * sendcount, stmp, (long long)n * sb, 0);
+    src = stmp;
+  }
+  if (!rc && !inplace && !rd.contig) {
+    if (!(rtmp = tmp_get(c, rb > 0 ? rb : 1))) rc = MPIGX_ERR_NO_MEM;
+    dst = rtmp;
+  }
+  if (!rc) rc = scatter_common(src, sb, nullptr, nullptr, MPIGX_BYTE, dst, inplace ? 0 : rb, MPIGX_BYTE, root, c);
+  if (!rc && rtmp) rc = pack_on(c, recvtype, recvbuf, recvcount, rtmp, rb, 1);
+  if (!rc) rc = finish(c);
+  if (stmp) tmp_put(c, stmp, 0);
+  if (rtmp) tmp_put(c, rtmp, 0);
+  return rc;
 }
 int mpigx_scatterv(const void* sendbuf, const int* sendcounts, const int* displs, int sendtype, void* recvbuf,
                    int recvcount, int recvtype, int root, mpigx_comm_t c) {
@@ -1224,7 +1424,7 @@ int mpigx_allgatherv(const void* sendbuf, int sendcount, int sendtype, void* rec
   if (!recvcounts || !displs) return MPIGX_ERR_ARG;
   const int n = c->n, r = c->rank;
   int rsz = 0;
-  if ((rc = mpigx_type_size(recvtype, &rsz))) return rc;
+  if ((rc = vsize(recvtype, &rsz))) return rc;
   const bool inplace = sendbuf == MPIGX_IN_PLACE;
   VSpec s;
   for (int p = 0; p < n; ++p) {
@@ -1263,10 +1463,10 @@ int mpigx_alltoallv(const void* sendbuf, const int* sendcounts, const int* sdisp
   const int n = c->n, r = c->rank;
   const bool inplace = sendbuf == MPIGX_IN_PLACE;
   int rsz = 0, ssz = 0;
-  if ((rc = mpigx_type_size(recvtype, &rsz))) return rc;
+  if ((rc = vsize(recvtype, &rsz))) return rc;
   if (!inplace) {
     if (!sendcounts || !sdispls) return MPIGX_ERR_ARG;
-    if ((rc = mpigx_type_size(sendtype, &ssz))) return rc;
+    if ((rc = vsize(sendtype, &ssz))) return rc;
   }
   VSpec s;
   s.ncopy = n;
@@ -1286,9 +1486,25 @@ int mpigx_alltoallv(const void* sendbuf, const int* sendcounts, const int* sdisp
   return vexchange(c, s);
 }
 
+// Reductions over a derived type: only contiguous runs of ONE predefined type
+// (MPI allows predefined ops on such types; they reduce element-wise).
+static int lower_reduce_type(int* datatype, int* count) {
+  if (!derived(*datatype)) return MPIGX_SUCCESS;
+  rt::TypeDesc d;
+  if (rt::type_info(*datatype, &d)) return MPIGX_ERR_TYPE;
+  const int bs = rt::dtype_size(d.basic);
+  if (!d.contig || d.basic == 0 || bs <= 0 || d.size % bs) return MPIGX_ERR_TYPE;
+  const long long n = (long long)*count * (d.size / bs);
+  if (n > 0x7fffffff) return MPIGX_ERR_COUNT;
+  *datatype = d.basic;
+  *count = (int)n;
+  return MPIGX_SUCCESS;
+}
+
 int mpigx_allreduce(const void* sendbuf, void* recvbuf, int count, int datatype, int op, mpigx_comm_t c) {
   int rc = check_comm(c);
   if (rc) return rc;
+  if ((rc = lower_reduce_type(&datatype, &count))) return rc;
   const TypeInfo* t;
   int oc;
   if ((rc = validate(datatype, op, &t, &oc))) return rc;
@@ -1303,6 +1519,7 @@ int mpigx_allreduce(const void* sendbuf, void* recvbuf, int count, int datatype,
 int mpigx_reduce(const void* sendbuf, void* recvbuf, int count, int datatype, int op, int root, mpigx_comm_t c) {
   int rc = check_comm(c);
   if (rc) return rc;
+  if ((rc = lower_reduce_type(&datatype, &count))) return rc;
   const TypeInfo* t;
   int oc;
   if ((rc = validate(datatype, op, &t, &oc))) return rc;
@@ -1321,6 +1538,7 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
                        int exclusive) {
   int rc = check_comm(c);
   if (rc) return rc;
+  if ((rc = lower_reduce_type(&datatype, &count))) return rc;
   const TypeInfo* t;
   int oc;
   if ((rc = validate(datatype, op, &t, &oc))) return rc;

@@ -90,6 +90,12 @@ struct Req {
   bool cancelled = false;
   bool detached = false;  // MPI_Request_free'd before completion
   int err = MPIGX_SUCCESS;
+  // derived datatypes (types.cpp): the send side travels packed from a pooled
+  // temporary; a non-contiguous receive is unpacked straight from the peer
+  char* pack_tmp = nullptr;
+  long long pack_cap = 0;
+  int rtype = 0;          // receive: derived type to unpack into (0: contiguous bytes)
+  long long rcount = 0;
 };
 
 std::vector<Req*> g_reqs;  // handle & kReqMask -> request
@@ -144,6 +150,7 @@ struct P2PState {
   std::vector<Req*> batch;        // pulls matched, not yet launched
   std::vector<Req*> detached;     // freed by the user, still in flight
   std::vector<hipEvent_t> evpool;
+  std::vector<std::pair<long long, char*>> packpool;  // free send-pack temporaries (hipMalloc, IPC-exportable)
   P2PMailbox* local = nullptr;    // single-rank communicator (no shm block)
 };
 }  // namespace mpigx
@@ -186,7 +193,36 @@ void put_event(P2PState* P, hipEvent_t& e) {
   e = nullptr;
 }
 
+char* pack_get(P2PState* P, long long bytes, long long* cap) {
+  size_t best = P->packpool.size();
+  for (size_t i = 0; i < P->packpool.size(); ++i)
+    if (P->packpool[i].first >= bytes && (best == P->packpool.size() || P->packpool[i].first < P->packpool[best].first))
+      best = i;
+  if (best < P->packpool.size()) {
+    char* p = P->packpool[best].second;
+    *cap = P->packpool[best].first;
+    P->packpool.erase(P->packpool.begin() + best);
+    return p;
+  }
+  const long long c = (bytes + (1 << 20) - 1) & ~((1ll << 20) - 1);
+  char* p = nullptr;
+  if (hipMalloc(&p, c) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  *cap = c;
+  return p;
+}
+
+// A completed send's temporary goes back to the pool (its exported handle and
+// the receiver's import stay valid for the next message using it).
+void pack_put(Req* r) {
+  if (r->pack_tmp && r->c && r->c->p2p) r->c->p2p->packpool.push_back({r->pack_cap, r->pack_tmp});
+  r->pack_tmp = nullptr;
+}
+
 void release(Req* r, int* handle) {
+  pack_put(r);
   if (r->c && r->c->p2p) {
     put_event(r->c->p2p, r->ready);
     put_event(r->c->p2p, r->done_ev);
@@ -246,6 +282,25 @@ void fail_pull(P2PState* P, Req* r) {
 // One xfer_kernel launch per <= kMaxXfer matched messages.
 void flush(mpigx_comm* c) {
   P2PState* P = c->p2p;
+  // non-contiguous receives: one unpack kernel each, reading the peer's
+  // packed bytes over xGMI and scattering them into the typed buffer
+  for (size_t k = 0; k < P->batch.size();) {
+    Req* r = P->batch[k];
+    if (!r->rtype) {
+      ++k;
+      continue;
+    }
+    P->batch.erase(P->batch.begin() + k);
+    bool ok = !r->ready || hipStreamWaitEvent(P->xs, r->ready, 0) == hipSuccess;
+    ok = ok && rt::type_pack(r->rtype, r->rbuf, r->rcount, (void*)r->xsrc, r->xlen, 1, c->device, P->xs) == 0;
+    r->done_ev = ok ? get_event(P) : nullptr;
+    if (!ok || !r->done_ev || hipEventRecord(r->done_ev, P->xs) != hipSuccess) {
+      (void)hipGetLastError();
+      fail_pull(P, r);
+      continue;
+    }
+    P->inflight.push_back(r);
+  }
   size_t i = 0;
   while (i < P->batch.size()) {
     const size_t m = std::min(P->batch.size() - i, (size_t)kMaxXfer);
@@ -362,6 +417,7 @@ bool complete(Req* r) {
   if (r->kind == K_SEND && r->state == S_POSTED &&
       r->env->done.load(std::memory_order_acquire) >= r->seq + 1) {
     r->state = S_DONE;
+    pack_put(r);
     return true;
   }
   return false;
@@ -388,13 +444,12 @@ void progress(mpigx_comm* c) {
   }
 }
 
-int check_common(mpigx_comm* c, const void* buf, int count, int datatype, int* esize) {
+int check_common(mpigx_comm* c, const void* buf, int count, int datatype, rt::TypeDesc* d) {
   int rc = rt::comm_check(c);
   if (rc) return rc;
   if (count < 0) return MPIGX_ERR_COUNT;
-  *esize = rt::dtype_size(datatype);
-  if (*esize < 0) return MPIGX_ERR_TYPE;
-  if (!buf && count > 0) return MPIGX_ERR_BUFFER;
+  if (rt::type_info(datatype, d)) return MPIGX_ERR_TYPE;
+  if (!buf && count > 0 && d->size > 0) return MPIGX_ERR_BUFFER;
   return MPIGX_SUCCESS;
 }
 
@@ -473,6 +528,7 @@ void p2p_destroy(mpigx_comm* c) {
     delete r;
   }
   for (hipEvent_t e : P->evpool) (void)hipEventDestroy(e);
+  for (auto& b : P->packpool) (void)hipFree(b.second);
   (void)hipStreamDestroy(P->xs);
   delete P->local;
   delete P;
@@ -489,7 +545,8 @@ extern "C" {
 int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpigx_comm_t c,
                 mpigx_request_t* request) {
   if (!request) return MPIGX_ERR_ARG;
-  int es, rc = check_common(c, buf, count, datatype, &es);
+  rt::TypeDesc td;
+  int rc = check_common(c, buf, count, datatype, &td);
   if (rc) return rc;
   if (dest != MPIGX_PROC_NULL && (dest < 0 || dest >= c->n)) return MPIGX_ERR_RANK;
   if (tag < 0 || tag > MPIGX_TAG_UB) return MPIGX_ERR_TAG;
@@ -501,13 +558,26 @@ int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpi
   r->peer = dest;
   r->tag = tag;
   r->sbuf = (const char*)buf;
-  r->bytes = (long long)count * es;
+  r->bytes = (long long)count * td.size;
   if (dest == MPIGX_PROC_NULL) {
     r->state = S_DONE;
     *request = new_handle(r);
     return MPIGX_SUCCESS;
   }
   if (r->bytes > 0) {
+    if (!td.contig) {  // derived, non-contiguous: pack on device into a pooled temporary
+      r->pack_tmp = pack_get(P, r->bytes, &r->pack_cap);
+      if (!r->pack_tmp) {
+        delete r;
+        return MPIGX_ERR_NO_MEM;
+      }
+      if ((rc = rt::type_pack(datatype, buf, count, r->pack_tmp, r->bytes, 0, c->device, c->stream))) {
+        P->packpool.push_back({r->pack_cap, r->pack_tmp});
+        delete r;
+        return rc;
+      }
+      r->sbuf = r->pack_tmp;
+    }
     // the receiver reads the buffer asynchronously: it must hold its final
     // contents now (prior producers on the comm's stream have finished)
     if (hipStreamSynchronize(c->stream) != hipSuccess) {
@@ -515,7 +585,8 @@ int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpi
       delete r;
       return MPIGX_ERR_INTERN;
     }
-    if (dest != c->rank && !rt::export_buf(c, buf, &r->buf_id, &r->off, &r->h)) {
+    if (dest != c->rank && !rt::export_buf(c, r->sbuf, &r->buf_id, &r->off, &r->h)) {
+      pack_put(r);
       delete r;
       return MPIGX_ERR_BUFFER;  // not a device allocation that can be IPC-exported
     }
@@ -529,7 +600,8 @@ int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpi
 int mpigx_irecv(void* buf, int count, int datatype, int source, int tag, mpigx_comm_t c,
                 mpigx_request_t* request) {
   if (!request) return MPIGX_ERR_ARG;
-  int es, rc = check_common(c, buf, count, datatype, &es);
+  rt::TypeDesc td;
+  int rc = check_common(c, buf, count, datatype, &td);
   if (rc) return rc;
   if (source != MPIGX_PROC_NULL && source != MPIGX_ANY_SOURCE && (source < 0 || source >= c->n))
     return MPIGX_ERR_RANK;
@@ -542,7 +614,11 @@ int mpigx_irecv(void* buf, int count, int datatype, int source, int tag, mpigx_c
   r->peer = source;
   r->tag = tag;
   r->rbuf = (char*)buf;
-  r->bytes = (long long)count * es;
+  r->bytes = (long long)count * td.size;
+  if (!td.contig) {
+    r->rtype = datatype;
+    r->rcount = count;
+  }
   if (source == MPIGX_PROC_NULL) {
     r->has_status = true;
     set_status(&r->st, 0, MPIGX_PROC_NULL, MPIGX_ANY_TAG, false);
@@ -860,8 +936,9 @@ int mpigx_probe(int source, int tag, mpigx_comm_t c, mpigx_status_t* status) {
 
 int mpigx_get_count(const mpigx_status_t* status, int datatype, int* count) {
   if (!status || !count) return MPIGX_ERR_ARG;
-  const int es = mpigx::rt::dtype_size(datatype);
-  if (es < 0) return MPIGX_ERR_TYPE;
+  mpigx::rt::TypeDesc td;
+  if (mpigx::rt::type_info(datatype, &td)) return MPIGX_ERR_TYPE;
+  const long long es = td.size;
   const long long bytes =
       ((long long)(status->count_hi_and_cancelled >> 1) << 31) | (long long)(status->count_lo & 0x7fffffff);
   if (es == 0 || bytes % es != 0 || bytes / es > 0x7fffffff)

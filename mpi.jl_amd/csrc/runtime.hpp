@@ -149,6 +149,7 @@ struct mpigx_comm {
     hipIpcMemHandle_t h;
   };
   std::vector<LocalReg> lreg;
+  std::vector<std::pair<long long, char*>> tmp_free, tmp_used;  // derived-type pack temporaries
   std::vector<Import> imports;
   unsigned long long tick = 0;
   long long zc_min = 16ll << 20;  // bytes; 0 disables
@@ -191,6 +192,19 @@ int pull_fences();  // MPIGX_PULL_FENCES (default 1): coherent flag of p2p / RMA
 void p2p_progress(mpigx_comm* c);
 void p2p_sync(mpigx_comm* c);     // drain the transfer stream
 void p2p_destroy(mpigx_comm* c);
+// types.cpp
+struct TypeDesc {
+  long long size;    // packed bytes per element
+  long long extent;  // bytes between consecutive elements in memory
+  int basic;         // predefined type every byte belongs to (0: mixed)
+  bool derived;
+  bool contig;       // count elements = count*size contiguous bytes from the pointer
+};
+int type_info(int datatype, TypeDesc* d);  // MPIGX_ERR_TYPE for unknown / uncommitted
+// pack (unpack=0: typed -> contig) or unpack the first `bytes` packed bytes of
+// `count` elements; enqueued on `s` (device `device`)
+int type_pack(int datatype, const void* typed, long long count, void* contig, long long bytes, int unpack, int device,
+              hipStream_t s);
 // rma.cpp
 void rma_progress(mpigx_comm* c);
 void rma_destroy(mpigx_comm* c);

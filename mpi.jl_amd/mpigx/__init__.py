@@ -10,6 +10,7 @@ from ._lib import HEADER_PATH, LIB_PATH, lib
 from .api import *  # noqa: F401,F403
 from .p2p import *  # noqa: F401,F403
 from .rma import *  # noqa: F401,F403
+from .types import Types  # noqa: F401
 from .api import (COMM_WORLD, IN_PLACE, Barrier, Buffer, Comm, Datatype, MPIError, Op, error_string,
                   reduce_local_multi)
 

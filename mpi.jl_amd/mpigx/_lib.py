@@ -101,6 +101,21 @@ PROTOTYPES = {
     "mpigx_accumulate": (c_int, [c_void_p, c_int, c_int, c_int, c_longlong, c_int, c_int, c_int, c_void_p]),
     "mpigx_get_accumulate": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_longlong, c_int, c_int,
                                      c_int, c_void_p]),
+    # derived datatypes
+    "mpigx_type_contiguous": (c_int, [c_int, c_int, _IP]),
+    "mpigx_type_vector": (c_int, [c_int, c_int, c_int, c_int, _IP]),
+    "mpigx_type_create_hvector": (c_int, [c_int, c_int, c_longlong, c_int, _IP]),
+    "mpigx_type_create_subarray": (c_int, [c_int, _IP, _IP, _IP, c_int, c_int, _IP]),
+    "mpigx_type_create_struct": (c_int, [c_int, _IP, ctypes.POINTER(c_longlong), _IP, _IP]),
+    "mpigx_type_create_resized": (c_int, [c_int, c_longlong, c_longlong, _IP]),
+    "mpigx_type_commit": (c_int, [_IP]),
+    "mpigx_type_free": (c_int, [_IP]),
+    "mpigx_type_get_extent": (c_int, [c_int, ctypes.POINTER(c_longlong), ctypes.POINTER(c_longlong)]),
+    "mpigx_type_get_true_extent": (c_int, [c_int, ctypes.POINTER(c_longlong), ctypes.POINTER(c_longlong)]),
+    "mpigx_type_size_x": (c_int, [c_int, ctypes.POINTER(c_longlong)]),
+    "mpigx_pack_size": (c_int, [c_int, c_int, ctypes.POINTER(c_longlong)]),
+    "mpigx_pack": (c_int, [c_void_p, c_int, c_int, c_void_p, c_longlong, ctypes.POINTER(c_longlong), c_void_p]),
+    "mpigx_unpack": (c_int, [c_void_p, c_longlong, ctypes.POINTER(c_longlong), c_void_p, c_int, c_int, c_void_p]),
     "mpigx_malloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),
     "mpigx_free": (c_int, [c_void_p]),
     "mpigx_memcpy": (c_int, [c_void_p, c_void_p, c_size_t]),

@@ -72,17 +72,25 @@ def Error_class(code: int) -> int:
 # Datatype (src/datatypes.jl:16-60, 269-292)
 # ---------------------------------------------------------------------------
 class Datatype:
-    __slots__ = ("val", "name")
+    """`val`: the handle libmpigx takes (MPICH's predefined values; derived
+    types: libmpigx's own, types.cpp); `host_val`: the host libmpi handle of a
+    derived type (same value for predefined types)."""
+    __slots__ = ("val", "name", "host_val")
 
-    def __init__(self, T, name=None):
+    def __init__(self, T, name=None, host_val=None):
         if isinstance(T, Datatype):
-            self.val, self.name = T.val, T.name
+            self.val, self.name, self.host_val = T.val, T.name, T.host_val
             return
         if isinstance(T, int) and name is not None:
-            self.val, self.name = T, name
+            self.val, self.name, self.host_val = T, name, host_val
             return
         dt = _datatype_of(T)
-        self.val, self.name = dt.val, dt.name
+        self.val, self.name, self.host_val = dt.val, dt.name, dt.host_val
+
+    @property
+    def host(self):
+        """Handle for host libmpi."""
+        return self.val if self.host_val is None else self.host_val
 
     def __eq__(self, o):
         return isinstance(o, Datatype) and o.val == self.val
@@ -131,6 +139,9 @@ def _datatype_of(T) -> Datatype:
     if T is bool:
         return UINT8_T
     if isinstance(T, np.dtype) or (isinstance(T, type) and issubclass(T, np.generic)):
+        if np.dtype(T).fields is not None or np.dtype(T).kind == "V":
+            from .types import struct_datatype  # isbits structs / primitive types (datatypes.jl:269-316)
+            return struct_datatype(np.dtype(T))
         h = hostmpi.HANDLE_OF_NP.get(np.dtype(T))
         if h is None:
             raise TypeError(f"no MPI datatype for {T!r}")
@@ -244,6 +255,12 @@ class Buffer:
         if isinstance(data, Buffer):
             self.data, self.count, self.datatype = data.data, data.count, data.datatype
             return
+        if count is None and datatype is None and _noncontiguous(data):
+            # buffers.jl:104-117: strided / dense sub-arrays become one
+            # element of a vector / subarray datatype
+            from .types import view_buffer
+            self.data, self.count, self.datatype = view_buffer(data)
+            return
         self.data = data
         self.count = int(count if count is not None else _len(data))
         self.datatype = Datatype(datatype if datatype is not None else data.dtype)
@@ -257,11 +274,20 @@ def _is_host(buf):
     return isinstance(_unwrap(buf), np.ndarray)
 
 
+def _noncontiguous(a):
+    if isinstance(a, np.ndarray):
+        return not a.flags.c_contiguous
+    return hasattr(a, "is_contiguous") and not a.is_contiguous()
+
+
 def _ptr(buf):
     if buf is None:
         return None
     if buf is IN_PLACE:
         return _IN_PLACE_PTR
+    if isinstance(buf, Buffer) and _noncontiguous(buf.data):  # typed by its datatype
+        d = buf.data
+        return ctypes.c_void_p(d.ctypes.data if isinstance(d, np.ndarray) else d.data_ptr())
     b = _unwrap(buf)
     if isinstance(b, np.ndarray):
         if not b.flags.c_contiguous:
@@ -287,8 +313,8 @@ def _eltype(buf):
 
 
 def _assert_minlength(buf, count):
-    """buffers.jl:25-31: only array buffers are checked."""
-    if buf is not None and buf is not IN_PLACE:
+    """buffers.jl:25-31: only array buffers are checked (not MPI.Buffer)."""
+    if buf is not None and buf is not IN_PLACE and not isinstance(buf, Buffer):
         assert _len(buf) >= count, f"buffer length {_len(buf)} < count {count}"
 
 
@@ -521,7 +547,8 @@ def _call(coll, buf, comm, *args):
     if _is_host(buf):
         if comm.host is None:
             raise TypeError("host buffers need host libmpi (start the ranks with mpiexec)")
-        rc = getattr(hostmpi.lib(), "MPI_" + coll)(*args, comm.host)
+        from .types import _host_args  # derived datatypes have their own host handles
+        rc = getattr(hostmpi.lib(), "MPI_" + coll)(*_host_args(args), comm.host)
     else:
         if not comm.val:
             raise TypeError("device buffers need a ROCm device")
@@ -560,6 +587,15 @@ def Bcast_(buf, *args):
     return buf
 
 
+def _side(buf, count, T):
+    """(count, datatype handle) one side of a collective passes: an explicit
+    MPI.Buffer carries its own (count, datatype) — e.g. a strided view's
+    vector type — otherwise the wrapper's count and element type."""
+    if isinstance(buf, Buffer):
+        return int(buf.count), buf.datatype.val
+    return int(count), T.val
+
+
 def Allgather_(*args):
     """Allgather!(sendbuf, recvbuf, count, comm) / Allgather!(sendrecvbuf, count, comm)
     — collective.jl:295-311."""
@@ -571,7 +607,8 @@ def Allgather_(*args):
     _assert_minlength(recvbuf, count * Comm_size(comm))
     _assert_minlength(sendbuf, count)
     T = _eltype(recvbuf)
-    _call("Allgather", recvbuf, comm, _ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val)
+    _call("Allgather", recvbuf, comm, _ptr(sendbuf), *_side(sendbuf, count, T), _ptr(recvbuf),
+          *_side(recvbuf, count, T))
     return recvbuf
 
 
@@ -600,10 +637,11 @@ def Alltoall_(*args):
     buflength = count * Comm_size(comm)
     _assert_minlength(recvbuf, buflength)
     _assert_minlength(sendbuf, buflength)
-    if sendbuf is not IN_PLACE:
+    if sendbuf is not IN_PLACE and not isinstance(sendbuf, Buffer):
         assert _eltype(sendbuf) == _eltype(recvbuf)
     T = _eltype(recvbuf)
-    _call("Alltoall", recvbuf, comm, _ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val)
+    _call("Alltoall", recvbuf, comm, _ptr(sendbuf), *_side(sendbuf, count, T), _ptr(recvbuf),
+          *_side(recvbuf, count, T))
     return recvbuf
 
 
@@ -646,7 +684,8 @@ def Scatter_(sendbuf, recvbuf, *args):
     _assert_minlength(recvbuf, count)
     T = _eltype(sendbuf) if recvbuf is IN_PLACE else _eltype(recvbuf)
     data = sendbuf if recvbuf is IN_PLACE or recvbuf is None else recvbuf
-    _call("Scatter", data, comm, _ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val, int(root))
+    _call("Scatter", data, comm, _ptr(sendbuf), *_side(sendbuf, count, T), _ptr(recvbuf), *_side(recvbuf, count, T),
+          int(root))
     return recvbuf
 
 
@@ -693,7 +732,8 @@ def Gather_(sendbuf, recvbuf, *args):
     _assert_minlength(sendbuf, count)
     T = _eltype(recvbuf) if sendbuf is IN_PLACE else _eltype(sendbuf)
     data = recvbuf if sendbuf is IN_PLACE else sendbuf
-    _call("Gather", data, comm, _ptr(sendbuf), int(count), T.val, _ptr(recvbuf), int(count), T.val, int(root))
+    _call("Gather", data, comm, _ptr(sendbuf), *_side(sendbuf, count, T), _ptr(recvbuf), *_side(recvbuf, count, T),
+          int(root))
     return recvbuf if isroot else None
 
 

@@ -120,7 +120,12 @@ def _be(backend):
 
 
 def _fn(backend, name):
-    return getattr(_be(backend), ("mpigx_" + name.lower()) if backend == "dev" else ("MPI_" + name))
+    f = getattr(_be(backend), ("mpigx_" + name.lower()) if backend == "dev" else ("MPI_" + name))
+    if backend == "dev":
+        return f
+    from .types import _host_args  # derived datatypes have their own host handles
+
+    return lambda *a: f(*_host_args(a))
 
 
 def free_request(req: Request):
