@@ -383,6 +383,24 @@ int mpigx_pack(const void *inbuf, int incount, int datatype, void *outbuf, long 
 int mpigx_unpack(const void *inbuf, long long insize, long long *position, void *outbuf, int outcount,
                  int datatype, void *stream);
 
+/* ---- user-defined ops (operators.jl:56-88 OpWrapper) --
+ * MPI_Op_create analogues.  Handles live in MPICH's user-op space
+ * (0x98000000 | index) and are accepted by Allreduce / Reduce / Scan /
+ * Exscan for predefined and contiguous derived types.  The engine gathers
+ * the contributions with its own kernels and folds in rank order,
+ * inout = x_q (op) inout from the highest contributing rank down.
+ *   host callback   — MPI_User_function on HOST copies (what MPI.jl's
+ *                     @cfunction(OpWrapper) is); operands staged via pinned memory
+ *   device callback — device pointers + the comm's stream (hipStream_t as
+ *                     void*); the callee enqueues its own kernels. */
+typedef void(mpigx_user_function)(void *invec, void *inoutvec, int *len, int *datatype);
+typedef void(mpigx_device_function)(const void *invec, void *inoutvec, long long len, int datatype,
+                                    void *stream);
+int mpigx_op_create(mpigx_user_function *user_fn, int commute, int *op);
+int mpigx_op_create_device(mpigx_device_function *device_fn, int commute, int *op);
+int mpigx_op_free(int *op);
+int mpigx_op_commutative(int op, int *commute);
+
 /* ---- device buffers (north-star subsystem 1: the ROCBuffer backing) ----- */
 int mpigx_malloc(void **ptr, size_t bytes);
 int mpigx_free(void *ptr);

@@ -1486,6 +1486,96 @@ int mpigx_alltoallv(const void* sendbuf, const int* sendcounts, const int* sdisp
   return vexchange(c, s);
 }
 
+// ---------------------------------------------------------------------------
+// User-defined ops (operators.jl:56-88 OpWrapper, MPI_Op_create; SURVEY §8f
+// row 4).  Two kinds of callback:
+//   host   (mpigx_op_create): MPI_User_function on HOST memory — what MPI.jl's
+//          @cfunction(OpWrapper) is; operands are staged device -> pinned host
+//   device (mpigx_op_create_device): called with DEVICE pointers and the
+//          comm's stream; it enqueues its own kernels (no staging)
+// Algorithm: the contributions are gathered with the engine's Allgather /
+// Gather kernels, then folded in rank order with inout = x_q (op) inout from
+// the highest rank down — x0 o (x1 o (... o x_{n-1})), MPI's canonical order
+// for non-commutative ops (identical for any associative op).
+// ---------------------------------------------------------------------------
+struct UserOp {
+  mpigx_user_function* host_fn;
+  mpigx_device_function* dev_fn;
+  int commute;
+};
+static std::vector<UserOp*> g_userops;
+constexpr int kUserOpTag = (int)0x98000000u;  // MPICH HANDLE_KIND_DIRECT | MPID_OP
+constexpr int kUserOpMask = 0x03ffffff;
+
+static UserOp* user_op(int h) {
+  if ((h & (int)0xfc000000u) != kUserOpTag) return nullptr;
+  const int i = h & kUserOpMask;
+  return i < (int)g_userops.size() ? g_userops[i] : nullptr;
+}
+
+// kind: 0 allreduce, 1 reduce, 2 scan, 3 exscan
+static int user_reduce(mpigx_comm* c, UserOp* u, const void* send, void* recv, int count, int datatype, int root, int kind) {
+  rt::TypeDesc d;
+  if (rt::type_info(datatype, &d) || !d.contig) return MPIGX_ERR_TYPE;
+  if (count < 0) return MPIGX_ERR_COUNT;
+  if (count == 0) return MPIGX_SUCCESS;
+  const int n = c->n, r = c->rank;
+  if (kind == 1 && (root < 0 || root >= n)) return MPIGX_ERR_ROOT;
+  const long long eb = (long long)count * d.size;
+  if (eb > 0x7fffffff) return MPIGX_ERR_COUNT;
+  const void* mine = send == MPIGX_IN_PLACE ? recv : send;
+  if (!mine || (!recv && (kind != 1 || r == root))) return MPIGX_ERR_BUFFER;
+  // every contribution needed here: all (allreduce), at the root (reduce), ranks <= r (scans)
+  char* all = tmp_get(c, (long long)n * eb);
+  if (!all) return MPIGX_ERR_NO_MEM;
+  int rc;
+  if (kind == 1)
+    rc = gather_common(mine, (int)eb, MPIGX_BYTE, all, (int)eb, nullptr, nullptr, MPIGX_BYTE, root, c);
+  else
+    rc = gather_like(mine, (int)eb, MPIGX_BYTE, all, (int)eb, MPIGX_BYTE, c, false);
+  int hi = n - 1;  // fold x_lo .. x_hi
+  bool skip = false;
+  if (kind == 1 && r != root) skip = true;
+  if (kind == 2) hi = r;
+  if (kind == 3) {
+    hi = r - 1;
+    if (r == 0) skip = true;  // rank 0's exscan result is untouched
+  }
+  if (!rc && !skip) {
+    int len = count, dt = datatype;
+    if (u->dev_fn) {
+      if (hipMemcpyAsync(recv, all + hi * eb, eb, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) rc = MPIGX_ERR_INTERN;
+      for (int q = hi - 1; !rc && q >= 0; --q) u->dev_fn(all + q * eb, recv, (long long)len, dt, (void*)c->stream);
+      c->unflagged = true;
+      if (!rc) rc = finish(c);
+      if (!rc && hipGetLastError() != hipSuccess) rc = MPIGX_ERR_OTHER;
+    } else {
+      char* h = nullptr;
+      if (hipHostMalloc((void**)&h, (size_t)(hi + 1) * eb, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        rc = MPIGX_ERR_NO_MEM;
+      } else {
+        if (hipMemcpyAsync(h, all, (size_t)(hi + 1) * eb, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess) {
+          (void)hipGetLastError();
+          rc = MPIGX_ERR_INTERN;
+        }
+        for (int q = hi - 1; !rc && q >= 0; --q) u->host_fn(h + q * eb, h + hi * eb, &len, &dt);
+        if (!rc && (hipMemcpyAsync(recv, h + hi * eb, eb, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+                    hipStreamSynchronize(c->stream) != hipSuccess)) {
+          (void)hipGetLastError();
+          rc = MPIGX_ERR_INTERN;
+        }
+        (void)hipHostFree(h);
+      }
+    }
+  } else if (!rc) {
+    rc = finish(c);
+  }
+  tmp_put(c, all, 0);
+  return rc;
+}
+
 // Reductions over a derived type: only contiguous runs of ONE predefined type
 // (MPI allows predefined ops on such types; they reduce element-wise).
 static int lower_reduce_type(int* datatype, int* count) {
@@ -1504,6 +1594,7 @@ static int lower_reduce_type(int* datatype, int* count) {
 int mpigx_allreduce(const void* sendbuf, void* recvbuf, int count, int datatype, int op, mpigx_comm_t c) {
   int rc = check_comm(c);
   if (rc) return rc;
+  if (UserOp* u = user_op(op)) return user_reduce(c, u, sendbuf, recvbuf, count, datatype, 0, 0);
   if ((rc = lower_reduce_type(&datatype, &count))) return rc;
   const TypeInfo* t;
   int oc;
@@ -1519,6 +1610,7 @@ int mpigx_allreduce(const void* sendbuf, void* recvbuf, int count, int datatype,
 int mpigx_reduce(const void* sendbuf, void* recvbuf, int count, int datatype, int op, int root, mpigx_comm_t c) {
   int rc = check_comm(c);
   if (rc) return rc;
+  if (UserOp* u = user_op(op)) return user_reduce(c, u, sendbuf, recvbuf, count, datatype, root, 1);
   if ((rc = lower_reduce_type(&datatype, &count))) return rc;
   const TypeInfo* t;
   int oc;
@@ -1538,6 +1630,7 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
                        int exclusive) {
   int rc = check_comm(c);
   if (rc) return rc;
+  if (UserOp* u = user_op(op)) return user_reduce(c, u, sendbuf, recvbuf, count, datatype, 0, exclusive ? 3 : 2);
   if ((rc = lower_reduce_type(&datatype, &count))) return rc;
   const TypeInfo* t;
   int oc;
@@ -1629,6 +1722,38 @@ int mpigx_reduce_local(const void* inbuf, void* inoutbuf, int count, int datatyp
   int rc = mpigx_reduce_local_multi(ptrs, 2, inoutbuf, count, datatype, op, MPIGX_ORDER_LINEAR, nullptr);
   if (rc) return rc;
   HIPCK(hipStreamSynchronize(nullptr));
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_op_create(mpigx_user_function* fn, int commute, int* op) {
+  if (!fn || !op) return MPIGX_ERR_ARG;
+  g_userops.push_back(new UserOp{fn, nullptr, commute});
+  *op = kUserOpTag | (int)(g_userops.size() - 1);
+  return MPIGX_SUCCESS;
+}
+int mpigx_op_create_device(mpigx_device_function* fn, int commute, int* op) {
+  if (!fn || !op) return MPIGX_ERR_ARG;
+  g_userops.push_back(new UserOp{nullptr, fn, commute});
+  *op = kUserOpTag | (int)(g_userops.size() - 1);
+  return MPIGX_SUCCESS;
+}
+int mpigx_op_free(int* op) {
+  if (!op) return MPIGX_ERR_ARG;
+  UserOp* u = user_op(*op);
+  if (!u) return MPIGX_ERR_OP;  // predefined ops cannot be freed
+  g_userops[*op & kUserOpMask] = nullptr;
+  delete u;
+  *op = 0x18000000;  // MPI_OP_NULL
+  return MPIGX_SUCCESS;
+}
+int mpigx_op_commutative(int op, int* commute) {
+  if (!commute) return MPIGX_ERR_ARG;
+  if (UserOp* u = user_op(op)) {
+    *commute = u->commute;
+    return MPIGX_SUCCESS;
+  }
+  if (op_code(op) == O_NONE) return MPIGX_ERR_OP;
+  *commute = 1;
   return MPIGX_SUCCESS;
 }
 

@@ -25,6 +25,9 @@ class UniqueId(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]
 
 
+USER_FN = ctypes.CFUNCTYPE(None, c_void_p, c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int))
+DEVICE_FN = ctypes.CFUNCTYPE(None, c_void_p, c_void_p, c_longlong, c_int, c_void_p)
+
 # name -> (restype, argtypes)
 PROTOTYPES = {
     "mpigx_get_version": (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
@@ -116,6 +119,11 @@ PROTOTYPES = {
     "mpigx_pack_size": (c_int, [c_int, c_int, ctypes.POINTER(c_longlong)]),
     "mpigx_pack": (c_int, [c_void_p, c_int, c_int, c_void_p, c_longlong, ctypes.POINTER(c_longlong), c_void_p]),
     "mpigx_unpack": (c_int, [c_void_p, c_longlong, ctypes.POINTER(c_longlong), c_void_p, c_int, c_int, c_void_p]),
+    # user-defined ops
+    "mpigx_op_create": (c_int, [USER_FN, c_int, _IP]),
+    "mpigx_op_create_device": (c_int, [DEVICE_FN, c_int, _IP]),
+    "mpigx_op_free": (c_int, [_IP]),
+    "mpigx_op_commutative": (c_int, [c_int, _IP]),
     "mpigx_malloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),
     "mpigx_free": (c_int, [c_void_p]),
     "mpigx_memcpy": (c_int, [c_void_p, c_void_p, c_size_t]),

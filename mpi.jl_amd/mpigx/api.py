@@ -558,10 +558,43 @@ def _call(coll, buf, comm, *args):
 
 
 def _op_val(opx, buf):
-    """Built-in handle, or (host only) an MPI_Op_create'd user function."""
+    """Built-in handle, or an MPI_Op_create'd user function: libmpi's for host
+    buffers, libmpigx's device-callback op for device buffers."""
     if opx.val is not None:
         return opx.val
-    return hostmpi.user_op(opx.fn, _unwrap(buf).dtype, opx.iscommutative)
+    if _is_host(buf):
+        return hostmpi.user_op(opx.fn, _unwrap(buf).dtype, opx.iscommutative)
+    return _device_user_op(opx, buf)
+
+
+_DEV_OPS = {}  # (function, torch dtype, commute) -> (op handle, ctypes callback)
+
+
+def _device_user_op(opx, buf):
+    """operators.jl:56-88 on device: `inout[i] = f(in[i], inout[i])` as torch
+    ops on the device pointers libmpigx hands the callback (enqueued on the
+    communicator's stream, which is torch's current stream)."""
+    from ._lib import DEVICE_FN
+    from .rma import _dlpack_wrap
+    b = _unwrap(buf)
+    tdt, dev = b.dtype, b.device.index
+    key = (opx.fn, tdt, bool(opx.iscommutative))
+    if key in _DEV_OPS:
+        return _DEV_OPS[key][0]
+    fn = opx.fn
+
+    def cb(inp, inout, n, dt, stream):
+        sz = ctypes.c_longlong(0)  # bytes per element of the (maybe derived) datatype
+        lib().mpigx_type_size_x(dt, ctypes.byref(sz))
+        a = _dlpack_wrap(inp, np.dtype(np.uint8), (n * sz.value,), dev).view(tdt)
+        y = _dlpack_wrap(inout, np.dtype(np.uint8), (n * sz.value,), dev).view(tdt)
+        y.copy_(fn(a, y))
+
+    f = DEVICE_FN(cb)
+    h = ctypes.c_int(0)
+    _check(lib().mpigx_op_create_device(f, int(bool(opx.iscommutative)), ctypes.byref(h)))
+    _DEV_OPS[key] = (h.value, f)
+    return h.value
 
 
 # ---------------------------------------------------------------------------
@@ -836,39 +869,6 @@ def _item(x):
     return x[0].item() if isinstance(x, np.ndarray) else x.item()
 
 
-def _user_fold(xs, fn):
-    """OpWrapper semantics (operators.jl:60-69): inout = f(in, inout), with the
-    lower rank as `in`; rank-ordered, so associativity suffices."""
-    acc = xs[0]
-    for x in xs[1:]:
-        acc = fn(acc, x)
-    return acc
-
-
-def _user_collective(kind, sendbuf, recvbuf, count, op, root, comm):
-    """Non-builtin Op on device buffers: gather the operands with the engine's
-    Allgather, fold with the user function as device tensor ops."""
-    torch = _torch()
-    n, r = Comm_size(comm), Comm_rank(comm)
-    src = recvbuf if sendbuf is IN_PLACE else sendbuf
-    flat = src.reshape(-1)[:count].contiguous()
-    g = torch.empty(n * count, dtype=flat.dtype, device=flat.device)
-    Allgather_(flat, g, count, comm)
-    xs = list(g.view(n, count).unbind(0))
-    if kind in ("allreduce", "reduce"):
-        if kind == "reduce" and r != root:
-            return recvbuf
-        res = _user_fold(xs, op.fn)
-    elif kind == "scan":
-        res = _user_fold(xs[: r + 1], op.fn)
-    else:  # exscan
-        if r == 0:
-            return recvbuf
-        res = _user_fold(xs[:r], op.fn)
-    recvbuf.reshape(-1)[:count].copy_(res.to(recvbuf.dtype))
-    return recvbuf
-
-
 def Reduce_(*args):
     """Reduce!(sendbuf, recvbuf, count, op, root, comm)          collective.jl:605
     Reduce!(sendbuf, recvbuf, op, root, comm)                     :626
@@ -890,8 +890,6 @@ def Reduce_(*args):
     data = recvbuf if sendbuf is IN_PLACE else sendbuf
     T = _eltype(data)
     opx = _as_op(op, _dtype(data))
-    if opx.val is None and not _is_host(data):
-        return _user_collective("reduce", sendbuf, recvbuf, count, opx, root, comm)
     _call("Reduce", data, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val, _op_val(opx, data), int(root))
     return recvbuf
 
@@ -927,8 +925,6 @@ def Allreduce_(*args):
         assert _eltype(sendbuf) == _eltype(recvbuf)
     T = _eltype(recvbuf)
     opx = _as_op(op, _dtype(recvbuf))
-    if opx.val is None and not _is_host(recvbuf):
-        return _user_collective("allreduce", sendbuf, recvbuf, count, opx, 0, comm)
     _call("Allreduce", recvbuf, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val, _op_val(opx, recvbuf))
     return recvbuf
 
@@ -963,8 +959,6 @@ def _scan_common(args, exclusive):
     sendbuf, recvbuf, count, op, comm = _scan_dispatch(args)
     T = _eltype(recvbuf)
     opx = _as_op(op, _dtype(recvbuf))
-    if opx.val is None and not _is_host(recvbuf):
-        return _user_collective("exscan" if exclusive else "scan", sendbuf, recvbuf, count, opx, 0, comm)
     _call("Exscan" if exclusive else "Scan", recvbuf, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val,
           _op_val(opx, recvbuf))
     return recvbuf

@@ -96,9 +96,11 @@ def dtype_handle(a):
 def user_op(fn, npdt, commute=False):
     """MPI_Op_create over a Python function (operators.jl:72-88)."""
     def cb(invec, inoutvec, plen, pdt):
-        n = plen[0]
-        a = np.ctypeslib.as_array((ctypes.c_char * (n * np.dtype(npdt).itemsize)).from_address(invec)).view(npdt)
-        b = np.ctypeslib.as_array((ctypes.c_char * (n * np.dtype(npdt).itemsize)).from_address(inoutvec)).view(npdt)
+        sz = ctypes.c_int(0)  # bytes per element of the (maybe derived) datatype
+        lib().MPI_Type_size(pdt[0], ctypes.byref(sz))
+        nb = plen[0] * sz.value
+        a = np.ctypeslib.as_array((ctypes.c_char * nb).from_address(invec)).view(npdt)
+        b = np.ctypeslib.as_array((ctypes.c_char * nb).from_address(inoutvec)).view(npdt)
         b[:] = np.asarray(fn(a, b), dtype=npdt)
 
     f = _USER_FN(cb)

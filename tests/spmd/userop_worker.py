@@ -1,0 +1,135 @@
+"""User-defined ops (src/operators.jl:56-88, test/test_allreduce.jl:19-21,
+test/test_reduce.jl:43-49) on device buffers, recorded like the other
+scenario workers: the host run uses MPICH's MPI_Op_create (golden,
+tests/golden/userop_golden.json), the device run libmpigx's
+mpigx_op_create_device (torch callback on device pointers) and
+mpigx_op_create (MPI_User_function on host-staged copies) — all three must
+agree exactly.
+
+Ops: the reference's `(x, y) -> 2x + y - x` on Int64 (commutative in value),
+and affine-map composition on pairs (a, b) ~ x -> a*x + b over a contiguous
+derived type of 2 Int64 — associative, NOT commutative, so the rank order of
+the fold is visible."""
+import ctypes
+import json
+import os
+import sys
+import traceback
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "mpi.jl_amd"))
+
+import numpy as np  # noqa: E402
+
+import mpigx as MPI  # noqa: E402
+
+DEVICE = os.environ.get("MPIGX_TEST_ARRAYTYPE", "") == "ROCArray"
+HOSTCB = os.environ.get("USEROP_HOSTCB", "") == "1"  # device buffers, host-staged MPI_User_function
+if DEVICE:
+    import torch
+
+REC = []
+comm = MPI.Init()
+rank, n = MPI.Comm_rank(comm), MPI.Comm_size(comm)
+
+
+def dev(a):
+    a = np.ascontiguousarray(a)
+    if DEVICE:
+        return torch.from_numpy(a.copy()).to(f"cuda:{comm.device}")
+    return a.copy()
+
+
+def H(x):
+    if DEVICE:
+        torch.cuda.synchronize()
+        return x.cpu().numpy()
+    return np.array(x, copy=True)
+
+
+def ref_fn(x, y):
+    return 2 * x + y - x
+
+
+def compose(x, y):
+    """in o inout for affine maps stored as (a, b) pairs."""
+    xv, yv = x.reshape(-1, 2), y.reshape(-1, 2)
+    a = xv[:, 0] * yv[:, 0]
+    b = xv[:, 0] * yv[:, 1] + xv[:, 1]
+    if DEVICE and not HOSTCB:
+        return torch.stack([a, b], dim=1).reshape(-1)
+    return np.stack([a, b], axis=1).reshape(-1)
+
+
+_keep = []
+
+
+def host_cb_op(fn):
+    """libmpigx host-callback op: MPI_User_function on host copies (int64 payload)."""
+    from mpigx._lib import USER_FN
+
+    def cb(invec, inoutvec, plen, pdt):
+        sz = ctypes.c_longlong(0)
+        MPI.lib().mpigx_type_size_x(pdt[0], ctypes.byref(sz))
+        nb = plen[0] * sz.value
+        a = np.ctypeslib.as_array((ctypes.c_char * nb).from_address(invec)).view(np.int64)
+        b = np.ctypeslib.as_array((ctypes.c_char * nb).from_address(inoutvec)).view(np.int64)
+        b[:] = fn(a, b)
+
+    f = USER_FN(cb)
+    h = ctypes.c_int(0)
+    assert MPI.lib().mpigx_op_create(f, 0, ctypes.byref(h)) == 0
+    _keep.append(f)
+    return MPI.Op(None, _val=h.value, _name="hostcb")
+
+
+def op_of(fn):
+    return host_cb_op(fn) if HOSTCB else MPI.Op(fn, np.int64)
+
+
+def cases():
+    # test_allreduce.jl's custom op on 3-, 9- and 27-element arrays
+    opr = op_of(ref_fn)
+    for shape in ((3,), (3, 3), (3, 3, 3)):
+        x = dev(np.arange(1, int(np.prod(shape)) + 1, dtype=np.int64).reshape(shape))
+        y = dev(np.zeros(shape, np.int64))
+        MPI.Allreduce_(x, y, opr, comm)
+        REC.append({"case": "allreduce_ref", "shape": list(shape), "y": H(y).reshape(-1).tolist()})
+    # Reduce to the last rank (test_reduce.jl root = sz-1)
+    x = dev(np.arange(5, dtype=np.int64) * (rank + 1))
+    y = dev(np.zeros(5, np.int64))
+    MPI.Reduce_(x, y, opr, n - 1, comm)
+    if rank == n - 1:
+        REC.append({"case": "reduce_ref", "y": H(y).tolist()})
+    # non-commutative affine composition over a contiguous pair type
+    pair = MPI.Types.commit_(MPI.Types.create_contiguous(2, MPI.Datatype(np.int64)))
+    opc = op_of(compose)
+    rng = np.random.default_rng(rank + 17)
+    m = 6
+    v = np.stack([rng.choice([1, 2, -1, 3], m), rng.integers(-5, 6, m)], axis=1).astype(np.int64).reshape(-1)
+    x = dev(v)
+    for kind in ("Allreduce", "Scan", "Exscan"):
+        y = dev(np.full(2 * m, 7, np.int64))
+        getattr(MPI, kind + "_")(MPI.Buffer(x, m, pair), MPI.Buffer(y, m, pair), opc, comm)
+        REC.append({"case": kind.lower() + "_compose", "y": H(y).tolist()})
+    y = dev(np.full(2 * m, 7, np.int64))
+    MPI.Reduce_(MPI.Buffer(x, m, pair), MPI.Buffer(y, m, pair), opc, 0, comm)
+    if rank == 0:
+        REC.append({"case": "reduce_compose", "y": H(y).tolist()})
+    # IN_PLACE allreduce with the custom op
+    z = dev(np.arange(4, dtype=np.int64) + rank)
+    MPI.Allreduce_(z, opr, comm)
+    REC.append({"case": "allreduce_inplace_ref", "z": H(z).tolist()})
+
+
+failed = None
+try:
+    cases()
+    MPI.Barrier(comm)
+except Exception:  # noqa: BLE001
+    failed = traceback.format_exc()
+with open(f"{os.environ['UO_OUT']}.{rank}", "w") as f:
+    f.write(json.dumps({"rank": rank, "n": n, "device": DEVICE, "records": REC, "failed": failed}) + "\n")
+MPI.Finalize()
+sys.exit(1 if failed else 0)
