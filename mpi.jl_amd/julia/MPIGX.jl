@@ -285,6 +285,156 @@ function Cancel!(req::ROCRequest)
     nothing
 end
 
+# ---------------------------------------------------------------------------
+# one-sided (src/onesided.jl) on device windows.  libmpigx windows are
+# opaque pointers; ROCWin keeps them apart from MPI.Win so the reference's
+# host methods stay untouched.
+# ---------------------------------------------------------------------------
+import MPI: Win_create, Win_create_dynamic, Win_fence, Win_flush, Win_sync, Win_lock, Win_unlock,
+            Win_attach, Win_detach, Get, Put, Fetch_and_op, Accumulate, Get_accumulate, LockType
+
+mutable struct ROCWin
+    ptr::Ptr{Cvoid}
+    comm::Comm
+end
+function wfree(w::ROCWin)
+    if w.ptr != C_NULL
+        h = Ref(w.ptr)
+        @mpichk ccall((:mpigx_win_free, libmpigx), Cint, (Ptr{Ptr{Cvoid}},), h)
+        w.ptr = C_NULL
+    end
+end
+MPI.free(w::ROCWin) = wfree(w)
+
+# onesided.jl:24-34
+function Win_create(base::ROCBuffer{T}, comm::Comm; infokws...) where T
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    @mpichk ccall((:mpigx_win_create, libmpigx), Cint, (Ptr{Cvoid}, Clonglong, Cint, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                  base.ptr, length(base) * sizeof(T), sizeof(T), engine(comm), h)
+    w = ROCWin(h[], comm); finalizer(wfree, w); w
+end
+# onesided.jl:47-56 (device flavour: `Win_create_dynamic(ROCBuffer, comm)`)
+function Win_create_dynamic(::Type{ROCBuffer}, comm::Comm; kwargs...)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    @mpichk ccall((:mpigx_win_create_dynamic, libmpigx), Cint, (Ptr{Cvoid}, Ptr{Ptr{Cvoid}}), engine(comm), h)
+    w = ROCWin(h[], comm); finalizer(wfree, w); w
+end
+# onesided.jl:72-83 (device flavour): returns (win, device pointer)
+function Win_allocate_shared(::Type{ROCBuffer}, ::Type{T}, len::Int, comm::Comm; kwargs...) where T
+    h = Ref{Ptr{Cvoid}}(C_NULL); p = Ref{Ptr{T}}(C_NULL)
+    @mpichk ccall((:mpigx_win_allocate_shared, libmpigx), Cint,
+                  (Clonglong, Cint, Ptr{Cvoid}, Ptr{Ptr{T}}, Ptr{Ptr{Cvoid}}), len * sizeof(T), sizeof(T), engine(comm), p, h)
+    w = ROCWin(h[], comm); finalizer(wfree, w); (w, p[])
+end
+function Win_shared_query(w::ROCWin, owner_rank::Int)
+    len = Ref{Clonglong}(); du = Ref{Cint}(); p = Ref{Ptr{Cvoid}}()
+    @mpichk ccall((:mpigx_win_shared_query, libmpigx), Cint, (Ptr{Cvoid}, Cint, Ptr{Clonglong}, Ptr{Cint}, Ptr{Ptr{Cvoid}}),
+                  w.ptr, owner_rank, len, du, p)
+    len[], du[], p[]
+end
+Win_attach(w::ROCWin, base::ROCBuffer{T}) where T =
+    @mpichk ccall((:mpigx_win_attach, libmpigx), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Clonglong), w.ptr, base.ptr, sizeof(T) * length(base))
+Win_detach(w::ROCWin, base::ROCBuffer) =
+    @mpichk ccall((:mpigx_win_detach, libmpigx), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), w.ptr, base.ptr)
+# onesided.jl:124-148
+Win_fence(assert::Integer, w::ROCWin) = @mpichk ccall((:mpigx_win_fence, libmpigx), Cint, (Cint, Ptr{Cvoid}), assert, w.ptr)
+Win_flush(rank::Integer, w::ROCWin) = @mpichk ccall((:mpigx_win_flush, libmpigx), Cint, (Cint, Ptr{Cvoid}), rank, w.ptr)
+Win_sync(w::ROCWin) = @mpichk ccall((:mpigx_win_sync, libmpigx), Cint, (Ptr{Cvoid},), w.ptr)
+Win_lock(lt::LockType, rank::Integer, assert::Integer, w::ROCWin) =
+    @mpichk ccall((:mpigx_win_lock, libmpigx), Cint, (Cint, Cint, Cint, Ptr{Cvoid}), lt.val, rank, assert, w.ptr)
+Win_unlock(rank::Integer, w::ROCWin) = @mpichk ccall((:mpigx_win_unlock, libmpigx), Cint, (Cint, Ptr{Cvoid}), rank, w.ptr)
+# onesided.jl:150-184 (device origin buffers)
+for (jl, c) in ((:Get, :mpigx_get), (:Put, :mpigx_put))
+    @eval function $jl(origin::ROCBuffer{T}, count::Integer, target_rank::Integer, target_disp::Integer, w::ROCWin) where T
+        @mpichk ccall(($(QuoteNode(c)), libmpigx), Cint,
+                      (MPIPtr, Cint, MPI_Datatype, Cint, Clonglong, Cint, MPI_Datatype, Ptr{Cvoid}),
+                      origin, count, Datatype(T), target_rank, target_disp, count, Datatype(T), w.ptr)
+    end
+    @eval $jl(origin::ROCBuffer, target_rank::Integer, w::ROCWin) = $jl(origin, length(origin), target_rank, 0, w)
+end
+# onesided.jl:186-195
+function Fetch_and_op(sourceval::ROCBuffer{T}, returnval::ROCBuffer{T}, target_rank::Integer,
+                      target_disp::Integer, op::Op, w::ROCWin) where T
+    @mpichk ccall((:mpigx_fetch_and_op, libmpigx), Cint,
+                  (MPIPtr, MPIPtr, MPI_Datatype, Cint, Clonglong, MPI_Op, Ptr{Cvoid}),
+                  sourceval, returnval, Datatype(T), target_rank, target_disp, op, w.ptr)
+end
+# onesided.jl:197-206
+function Accumulate(origin::ROCBuffer{T}, count::Integer, target_rank::Integer, target_disp::Integer,
+                    op::Op, w::ROCWin) where T
+    @mpichk ccall((:mpigx_accumulate, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, Cint, Clonglong, Cint, MPI_Datatype, MPI_Op, Ptr{Cvoid}),
+                  origin, count, Datatype(T), target_rank, target_disp, count, Datatype(T), op, w.ptr)
+end
+# onesided.jl:208-219
+function Get_accumulate(origin::ROCBuffer{T}, result::ROCBuffer{T}, count::Integer, target_rank::Integer,
+                        target_disp::Integer, op::Op, w::ROCWin) where T
+    @mpichk ccall((:mpigx_get_accumulate, libmpigx), Cint,
+                  (MPIPtr, Cint, MPI_Datatype, MPIPtr, Cint, MPI_Datatype, Cint, Clonglong, Cint, MPI_Datatype,
+                   MPI_Op, Ptr{Cvoid}),
+                  origin, count, Datatype(T), result, count, Datatype(T), target_rank, target_disp, count,
+                  Datatype(T), op, w.ptr)
+end
+
+# ---------------------------------------------------------------------------
+# derived datatypes for device buffers (datatypes.jl:62-318, buffers.jl:104-117):
+# libmpigx keeps its own type table (handles in MPICH's derived-type space),
+# so SubArrays of a ROCBuffer get libmpigx vector / subarray types.
+# ---------------------------------------------------------------------------
+module DevTypes
+    import ..MPIGX: libmpigx
+    import MPI: Datatype, MPI_Datatype, @mpichk
+    dt(v::Cint) = MPI._Datatype(v)
+    function create_vector(count, bl, stride, old::Datatype)
+        r = Ref{Cint}()
+        @mpichk ccall((:mpigx_type_vector, libmpigx), Cint, (Cint, Cint, Cint, Cint, Ptr{Cint}), count, bl, stride, old.val, r)
+        dt(r[])
+    end
+    function create_subarray(sizes, subsizes, offset, old::Datatype; rowmajor=false)
+        r = Ref{Cint}()
+        @mpichk ccall((:mpigx_type_create_subarray, libmpigx), Cint,
+                      (Cint, Ptr{Cint}, Ptr{Cint}, Ptr{Cint}, Cint, Cint, Ptr{Cint}),
+                      length(sizes), Cint[sizes...], Cint[subsizes...], Cint[offset...], rowmajor ? 56 : 57, old.val, r)
+        dt(r[])
+    end
+    function create_struct(bl, disp, types)
+        r = Ref{Cint}()
+        @mpichk ccall((:mpigx_type_create_struct, libmpigx), Cint, (Cint, Ptr{Cint}, Ptr{Clonglong}, Ptr{Cint}, Ptr{Cint}),
+                      length(bl), Cint[bl...], Clonglong[disp...], Cint[t.val for t in types], r)
+        dt(r[])
+    end
+    function commit!(d::Datatype)
+        r = Ref(d.val)
+        @mpichk ccall((:mpigx_type_commit, libmpigx), Cint, (Ptr{Cint},), r)
+        d
+    end
+end
+# buffers.jl:104-117 for views of device buffers
+function Buffer(sub::SubArray{T,1,<:ROCBuffer}) where T
+    stride1 = strides(sub)[1]
+    d = DevTypes.commit!(DevTypes.create_vector(length(sub), 1, stride1, Datatype(T)))
+    Buffer(sub, Cint(1), d)
+end
+function Buffer(sub::SubArray{T,N,<:ROCBuffer}) where {T,N}
+    d = DevTypes.commit!(DevTypes.create_subarray(size(parent(sub)), map(length, sub.indices),
+                                                  map(i -> first(i) - 1, sub.indices), Datatype(T)))
+    Buffer(parent(sub), Cint(1), d)
+end
+
+# ---------------------------------------------------------------------------
+# user-defined ops on device buffers (operators.jl:56-88): the reference's
+# OpWrapper becomes an MPI_User_function that libmpigx calls on host-staged
+# copies of the operands (mpigx_op_create).
+# ---------------------------------------------------------------------------
+function DeviceOp(f, ::Type{T}; iscommutative=false) where T
+    w = MPI.OpWrapper{typeof(f),T}(f)
+    fptr = @cfunction($w, Cvoid, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cint}, Ptr{MPI_Datatype}))
+    r = Ref{Cint}()
+    @mpichk ccall((:mpigx_op_create, libmpigx), Cint, (Ptr{Cvoid}, Cint, Ptr{Cint}), fptr, iscommutative, r)
+    op = MPI.Op(r[], fptr)  # keeps the closure alive like operators.jl:85
+    op
+end
+
 function __finalize()
     for h in values(ENGINE)
         ccall((:mpigx_comm_free, libmpigx), Cint, (Ptr{Cvoid},), h)
@@ -297,6 +447,6 @@ end
 # finalizer runs after them (environment.jl:37-62, refcount_inc/_dec).
 atexit(__finalize)
 
-export ROCBuffer, ROCRequest
+export ROCBuffer, ROCRequest, ROCWin, DeviceOp
 
 end # module
