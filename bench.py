@@ -13,7 +13,11 @@ step / wall time per step), roofline against HBM.
 
 N > 1 runs config 3 at 256 MiB: MPI.Allreduce!(SUM) of 256 MiB f32 per rank,
 blocking MPI semantics; value = busbw = S/t * 2(N-1)/N (nccl-tests), the max
-time over ranks, roofline against aggregate xGMI ingress.
+time over ranks, roofline against aggregate xGMI ingress.  The same line
+carries the Allreduce size sweep, the RCCL comparison, config 4
+(Bcast!/Allgather!/Alltoall! sweep), config 5 (Scan!/Exscan!/Reduce! on
+Int32/Int64 with BAND/BOR/MAX, bit-exact check) and the reference path
+(MPICH MPI_Allreduce, 8 ranks on the host cores) measured in the same run.
 
 Rank 0 prints ONE JSON line.  Inputs are synthetic, resident in HBM before
 timing.
@@ -42,6 +46,8 @@ def parse():
     p.add_argument("--nbuf", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-iters", type=int, default=30)
+    p.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison (N>1)")
+    p.add_argument("--no-extra", action="store_true", help="skip the config-4/5 blocks (N>1)")
     return p.parse_args()
 
 
@@ -69,6 +75,40 @@ def cpu_baseline_local(nbuf, mib, iters):
     t = (time.perf_counter() - t0) / 3
     return {"value": round((nbuf + 1) * cnt * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"numpy oracle, {nbuf} x {mib // 8} MiB f32 SUM, 3 calls"}
+
+
+def host_cpu():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"host_threads": os.cpu_count(), "usable_threads": len(os.sched_getaffinity(0)), "model": model}
+
+
+def cpu_reference_allreduce(ranks=8, mib=256, iters=3):
+    """The reference path on the host cores: MPICH 3.3.2 MPI_Allreduce(f32 SUM)
+    under `mpiexec -n ranks` (oracle/_ref/mpich_bench; the call MPI.jl makes at
+    collective.jl:698-700)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "mpich_bench")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    if not (os.path.exists(exe) and os.path.exists(mpiexec)):
+        return {"error": "MPICH harness not built (oracle/Makefile) or mpiexec missing"}
+    try:
+        out = subprocess.run([mpiexec, "-n", str(ranks), exe, "allreduce", str(mib), str(iters)],
+                             capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    if out.returncode != 0 or not line:
+        return {"error": (out.stderr or out.stdout)[-200:]}
+    j = json.loads(line[-1])
+    return {"ranks": ranks, "cores": min(ranks, os.cpu_count() or ranks), "mib": mib, "iters": iters,
+            "sec_per_call": j["sec_per_call"], "algbw_GBps": j["algbw_GBps"], "busbw_GBps": j["busbw_GBps"],
+            "kind": "reference", "impl": "MPICH 3.3.2 MPI_Allreduce f32 SUM, host buffers", **host_cpu()}
 
 
 def traffic_from_profiles(key):
@@ -159,6 +199,26 @@ def bench_local(args):
                 "bf16_SUM_GBps": time_variant(torch.bfloat16, MPI.SUM),
                 "bf16_MAX_GBps": time_variant(torch.bfloat16, MPI.MAX)}
 
+    # message-size sweep of the same kernel (f32 SUM, 8 inputs), kernel time
+    sweep = {}
+    for mib in (1, 4, 16, 64):
+        k = mib << 18
+        xs = [x[:k] for x in ins]
+        o = out[:k]
+        for _ in range(3):
+            MPI.reduce_local_multi(xs, o, MPI.SUM, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        e0.record(stream)
+        for _ in range(reps):
+            MPI.reduce_local_multi(xs, o, MPI.SUM, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / reps * 1e3
+        sweep[f"{mib}MiB"] = {"GBps": round((args.nbuf + 1) * k * 4 / (us / 1e6) / 1e9, 1), "us": round(us, 2)}
+    sweep[f"{args.mib}MiB"] = {"GBps": round(algo / (kern_ms / 1e3) / 1e9, 1), "us": round(kern_ms * 1e3, 2)}
+    cpu_ar = None if args.no_cpu_baseline else cpu_reference_allreduce()
+
     achieved = algo / (kern_ms / 1e3) / 1e9
     value = algo / wall / 1e9
     traffic = traffic_from_profiles("reduce_local_multi_f32_sum_8x256MiB")
@@ -178,6 +238,8 @@ def bench_local(args):
         "parity_sample_bit_exact": parity,
         "hbm_copy_peak_GBps_measured": round(copy_gbps, 1),
         "variants": variants,
+        "sweep_local_f32_sum": sweep,
+        "cpu_reference_allreduce_256MiB": cpu_ar,
     }
     print(json.dumps(res), flush=True)
 
@@ -264,14 +326,102 @@ def bench_allreduce(args):
             tw, _ = time_ar(nb, 10, 2)
             sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
         os.environ.pop("MPIGX_ALGO", None)
-    try:
-        ng = dist.new_group(backend="nccl")
-        for nb in sizes:
-            tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2,
-                            fn=lambda s_, r_: (r_.copy_(s_), dist.all_reduce(r_, group=ng)))
-            rccl[f"{nb >> 20}MiB"] = round(busbw(nb, tw), 1)
-    except Exception as e:  # noqa: BLE001
-        rccl = {"error": str(e)[:200]}
+    if args.no_rccl:
+        rccl = {"skipped": True}
+    else:
+        try:
+            ng = dist.new_group(backend="nccl")
+            for nb in sizes:
+                tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2,
+                                fn=lambda s_, r_: (r_.copy_(s_), dist.all_reduce(r_, group=ng)))
+                rccl[f"{nb >> 20}MiB"] = round(busbw(nb, tw), 1)
+        except Exception as e:  # noqa: BLE001
+            rccl = {"error": str(e)[:200]}
+
+    def time_call(call, steps, warmup):
+        for _ in range(warmup):
+            call()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        torch.cuda.synchronize()
+        (tw,) = tmax((time.perf_counter() - t0) / steps)
+        return tw
+
+    # config 4: Bcast! / Allgather! / Alltoall! f32 sweep (S = per-rank buffer
+    # for Bcast, total recv for Allgather, total send for Alltoall); busbw
+    # factors as nccl-tests: 1, (n-1)/n, (n-1)/n
+    cfg4 = {}
+    if not args.no_extra:
+        for nb in (64 << 10, 1 << 20, 16 << 20, 128 << 20, 512 << 20):
+            cnt = nb // 4
+            steps = 10 if nb <= (16 << 20) else 3
+            buf = torch.full((cnt,), float(rank), device=dev)
+            tb = time_call(lambda: MPI.Bcast_(buf, 0, comm), steps, 2)
+            okb = bool(torch.all(buf == 0).item())
+            per = cnt // n
+            src = torch.full((per,), float(rank), device=dev)
+            dst = torch.empty(per * n, device=dev)
+            tg = time_call(lambda: MPI.Allgather_(src, dst, per, comm), steps, 2)
+            okg = bool(torch.equal(dst, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per)))
+            a2s = torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) + 100 * rank
+            a2r = torch.empty_like(a2s)
+            ta = time_call(lambda: MPI.Alltoall_(a2s, a2r, per, comm), steps, 2)
+            oka = bool(torch.equal(a2r, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) * 100
+                                   + rank))
+            f = (n - 1) / n
+            cfg4[f"{nb >> 10}KiB"] = {
+                "bcast_busbw": round(nb / tb / 1e9, 2), "allgather_busbw": round(nb / tg / 1e9 * f, 2),
+                "alltoall_busbw": round(nb / ta / 1e9 * f, 2), "ok": okb and okg and oka}
+            del buf, src, dst, a2s, a2r
+
+    # config 5: Scan! / Exscan! / Reduce! with BAND/BOR/MAX on Int32/Int64,
+    # bit-exact against the fold of every rank's (regenerated) input
+    cfg5, cfg5_ok = {}, True
+    if not args.no_extra:
+        ops = (("BAND", MPI.BAND, torch.bitwise_and), ("BOR", MPI.BOR, torch.bitwise_or),
+               ("MAX", MPI.MAX, torch.maximum))
+        for tdt, lim in ((torch.int32, 1 << 31), (torch.int64, 1 << 62)):
+            for cnt in (1 << 10, 1 << 20, 64 << 20):
+                def gen(q):
+                    g = torch.Generator(device=dev).manual_seed(7000 + 31 * q + cnt)
+                    return torch.randint(-lim, lim, (cnt,), dtype=tdt, device=dev, generator=g)
+                xs = [gen(q) for q in range(n)]
+                mine = xs[rank]
+                for oname, op, fn in ops:
+                    pref = [xs[0]]
+                    for q in range(1, n):
+                        pref.append(fn(pref[-1], xs[q]))
+                    out = torch.zeros_like(mine)
+                    steps = 3 if cnt >= (64 << 20) else 5
+                    res = {}
+                    ts = time_call(lambda: MPI.Scan_(mine, out, op, comm), steps, 1)
+                    ok = bool(torch.equal(out, pref[rank]))
+                    res["scan_algbw"] = round(cnt * mine.element_size() / ts / 1e9, 2)
+                    out.zero_()
+                    te = time_call(lambda: MPI.Exscan_(mine, out, op, comm), steps, 1)
+                    ok &= rank == 0 or bool(torch.equal(out, pref[rank - 1]))
+                    res["exscan_algbw"] = round(cnt * mine.element_size() / te / 1e9, 2)
+                    root = n - 1
+                    rout = torch.zeros_like(mine) if rank == root else None
+                    tr = time_call(lambda: MPI.Reduce_(mine, rout, op, root, comm), steps, 1)
+                    if rank == root:
+                        ok &= bool(torch.equal(rout, pref[-1]))
+                    res["reduce_algbw"] = round(cnt * mine.element_size() / tr / 1e9, 2)
+                    (bad,) = tmax(0.0 if ok else 1.0)
+                    res["bit_exact"] = bad == 0.0
+                    cfg5_ok &= res["bit_exact"]
+                    cfg5[f"{str(tdt)[6:]}_{oname}_{cnt}"] = res
+                del xs, pref, mine, out
+
+    # the reference path on this box's host cores, same run (rank 0 only)
+    cpu_ar = None
+    if not args.no_cpu_baseline:
+        if rank == 0:
+            cpu_ar = cpu_reference_allreduce(8, args.mib, 3)
+        dist.barrier()
 
     value = busbw(S, t)
     ach = busbw(S, kern)
@@ -293,10 +443,13 @@ def bench_allreduce(args):
                                        if peak_meas else f"nominal {n - 1} x {XGMI_LINK_GBPS} GB/s",
                          "peak_nominal": peak_nom},
             "cpu_baseline": None,
+            "cpu_reference_allreduce": cpu_ar,
             "correct": ok,
             "xgmi_probe": probe,
             "sweep_mpigx_busbw": sweep,
             "rccl_busbw": rccl,
+            "config4_bcast_allgather_alltoall": cfg4,
+            "config5_scan_exscan_reduce": {"bit_exact_all": cfg5_ok, "cases": cfg5},
         }
         print(json.dumps(res), flush=True)
     MPI.Finalize()

@@ -47,7 +47,14 @@ enum FoldMode : int {
 };
 
 // Copy-kernel modes (Bcast / Allgather / Alltoall / Barrier).
-enum CopyMode : int { C_BCAST = 0, C_ALLGATHER = 1, C_ALLTOALL = 2, C_BARRIER = 3, C_PROBE_ALL = 4, C_PROBE_ONE = 5 };
+//   C_BCAST     : every non-root pulls the whole buffer from the root (small)
+//   C_BCAST_SAG : scatter + allgather — rank q pulls chunk q from the root, then
+//                 every rank pulls chunk p from rank p (large, n >= 3): each
+//                 xGMI link carries <= 2S/n instead of each root link carrying S
+enum CopyMode : int {
+  C_BCAST = 0, C_ALLGATHER = 1, C_ALLTOALL = 2, C_BARRIER = 3, C_PROBE_ALL = 4, C_PROBE_ONE = 5,
+  C_BCAST_SAG = 6
+};
 
 // Per-call view of the communicator, passed by value to every kernel.
 struct PeerView {
@@ -99,6 +106,7 @@ struct CopyArgs {
   long long slice;     // bytes per block slice (multiple of 16)
   long long total;     // user-buffer stride between rank blocks (bytes of one full block)
   long long sstride;   // alltoall: staging stride between rank blocks (bytes rounded up to 16)
+  long long chunk;     // bcast-sag: bytes per rank chunk (multiple of 16)
   const void* send;
   void* recv;
 };

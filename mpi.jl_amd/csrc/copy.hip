@@ -16,6 +16,13 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
   signal_done(A.pv);
 }
 
+// Slice b of chunk k of a chunked byte range: [k*chunk, (k+1)*chunk) ∩ [0,bytes).
+__device__ __forceinline__ void chunk_slice(const CopyArgs& A, int k, int b, long long* lo, long long* hi) {
+  const long long c0 = lmin((long long)k * A.chunk, A.bytes), c1 = lmin(c0 + A.chunk, A.bytes);
+  *lo = lmin(c0 + (long long)b * A.slice, c1);
+  *hi = lmin(*lo + A.slice, c1);
+}
+
 template <int NMAX>
 __device__ __forceinline__ void copy_body(const CopyArgs& A) {
   const PeerView& pv = A.pv;
@@ -60,6 +67,45 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
   char* dsts[NMAX];
   const char* srcs[NMAX];
   long long lens[NMAX];
+  if (A.mode == C_BCAST_SAG) {
+    // scatter + allgather (block b owns slice b of every chunk): the root
+    // stages everything; rank q pulls chunk q from the root into its own
+    // staging; then every non-root pulls chunk p from rank p (the root's
+    // chunk from the root, its own chunk locally).  Each root link carries
+    // 2S/n, every other link S/n, instead of S on each root link.
+    long long l, h;
+    if (r == A.root)
+      for (int k = 0; k < n; ++k) {
+        chunk_slice(A, k, b, &l, &h);
+        block_copy(mine + l, send + l, h - l);
+      }
+    if (!rank_barrier(pv, ep++)) return;
+    if (r != A.root) {
+      chunk_slice(A, r, b, &l, &h);
+      block_copy(mine + l, pv.stage[A.root] + l, h - l);
+    }
+    if (!rank_barrier(pv, ep++)) return;
+    if (r != A.root) {
+      int m = 0;
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j) {
+        dsts[j] = nullptr;
+        srcs[j] = nullptr;
+        lens[j] = 0;
+        if (j < n) {
+          const int p = (r + j) % n;
+          chunk_slice(A, p, b, &l, &h);
+          dsts[j] = recv + l;
+          srcs[j] = (p == r ? mine : pv.stage[p]) + l;
+          lens[j] = h - l;
+          m = j + 1;
+        }
+      }
+      block_gather<NMAX>(dsts, srcs, lens, m);
+    }
+    rank_barrier(pv, ep++);
+    return;
+  }
   if (A.mode == C_ALLGATHER) {
     block_copy(mine + lo, send + lo, len);
     if (!rank_barrier(pv, ep++)) return;

@@ -787,6 +787,7 @@ int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t*
   if (c->max_blocks > kMaxBlocks) c->max_blocks = kMaxBlocks;
   c->oneshot_max = env_ll("MPIGX_ONESHOT_MAX", 256 << 10);
   c->zc_min = env_ll("MPIGX_ZC_MIN", 16ll << 20);
+  c->bcast_sag_min = env_ll("MPIGX_BCAST_SAG_MIN", 256 << 10);
   c->zc_require = env_ll("MPIGX_ZC_REQUIRE", 0) != 0;
   // 8 KiB of message per block: 64 KiB one-shot drops 19.5 -> 6.7 us and
   // 1 MiB two-shot 31 -> 19 us vs 64 KiB per block (tools/latency.py, 2 ranks)
@@ -1071,21 +1072,36 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
   if (c->n == 1) return finish(c);
   const long long bytes = (long long)count * t->size;
   const long long round = (long long)(c->stage_bytes & ~(size_t)15);
+  // direct pull from the root (one barrier less) for small messages or two
+  // ranks; scatter + allgather when the root's links would be the bottleneck.
+  // The choice depends only on (bytes, n, env), identical on every rank.
+  const char* env = getenv("MPIGX_BCAST");
+  bool sag = c->n >= 3 && bytes >= c->bcast_sag_min;
+  if (env && !strcmp(env, "direct")) sag = false;
+  if (env && !strcmp(env, "sag")) sag = c->n >= 2;
   for (long long off = 0; off < bytes; off += round) {
     const long long len = bytes - off < round ? bytes - off : round;
     CopyArgs a;
     memset(&a, 0, sizeof a);
     a.pv = make_view(c);
-    a.mode = C_BCAST;
     a.root = root;
     a.bytes = len;
-    const int g = grid_for(c, len);
-    a.slice = rup(cdiv(len, g), 16);
     a.send = (const char*)buf + off;
     a.recv = (char*)buf + off;
+    int g;
+    if (sag) {
+      a.mode = C_BCAST_SAG;
+      a.chunk = rup(cdiv(len, c->n), 16);
+      g = grid_for(c, a.chunk);
+      a.slice = rup(cdiv(a.chunk, g), 16);
+    } else {
+      a.mode = C_BCAST;
+      g = grid_for(c, len);
+      a.slice = rup(cdiv(len, g), 16);
+    }
     HIPCK(launch_copy(dim3(g), c->stream, a));
     note_launch(c, a.pv, g);
-    c->epoch += 2;
+    c->epoch += sag ? 3 : 2;
   }
   return finish(c);
 }

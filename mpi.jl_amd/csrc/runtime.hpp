@@ -167,6 +167,7 @@ struct mpigx_comm {
   // tuning
   int max_blocks = 256;
   long long oneshot_max = 256 << 10;
+  long long bcast_sag_min = 256 << 10;  // Bcast: scatter+allgather from this size (n >= 3)
   long long bytes_per_block = 64 << 10;
   std::mutex mu;
 };

@@ -249,8 +249,17 @@ class Runner:
             ins1 = [x[:count] for x in ins]
             got = self.run("allgather", ins1, "FLOAT", None, count)
             self.check(same_bits(got, M.allgather(ins1)[r]), ("allgather", count))
-            got = self.run("bcast", ins1, "FLOAT", None, count, root=n - 1)
-            self.check(same_bits(got, ins1[n - 1]), ("bcast", count))
+            for algo in ("direct", "sag"):  # root pull vs scatter+allgather
+                os.environ["MPIGX_BCAST"] = algo
+                for root in sorted({0, n // 2, n - 1}):
+                    got = self.run("bcast", ins1, "FLOAT", None, count, root=root)
+                    self.check(same_bits(got, ins1[root]), ("bcast", algo, root, count))
+            os.environ.pop("MPIGX_BCAST", None)
+        # bytes that are not a multiple of 16 per chunk, default algorithm choice
+        for count in (262_145, 1_000_003):
+            ins1 = make("UINT8_T", "BXOR", n, count, 91 + count)
+            got = self.run("bcast", ins1, "UINT8_T", None, count, root=1 % n)
+            self.check(same_bits(got, ins1[1 % n]), ("bcast-u8", count))
 
     def linear_order(self):
         MPI.set_reduce_order(self.comm, 1)
