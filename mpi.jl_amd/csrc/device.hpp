@@ -260,12 +260,18 @@ __device__ __forceinline__ void fold_at(const FoldArgs& A, const T* const* src, 
     for (int w = 0; w < W; ++w) own[w] = 0;
     if constexpr (role_sensitive<OP, T>::v) {
       if (A.owner_mode) {
+        // Rabenseifner block of each element: one 64-bit division per vector,
+        // then step across the (rare) block boundaries inside the vector
         const unsigned pof2 = 1u << A.pof2_log;
+        const unsigned long long g0 = (unsigned long long)(A.gbase + e), bl = (unsigned long long)A.blk_len;
+        unsigned long long j = g0 / bl, next = (j + 1) * bl;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-          unsigned long long j = (unsigned long long)(A.gbase + e + w) / (unsigned long long)A.blk_len;
-          if (j > pof2 - 1) j = pof2 - 1;
-          own[w] = bitrev((unsigned)j, A.pof2_log);
+          while (g0 + w >= next) {
+            ++j;
+            next += bl;
+          }
+          own[w] = bitrev((unsigned)(j > pof2 - 1 ? pof2 - 1 : j), A.pof2_log);
         }
       }
     }
