@@ -297,6 +297,35 @@ def bench_allreduce(args):
     S = args.mib << 20
     t, kern = time_ar(S, args.steps, args.warmup)
 
+    # measured xGMI ingress/egress of my GPU over the same workload (SMU
+    # metrics, per link, KB; tools/xgmi_counters.py) vs the algorithmic
+    # 2S(n-1)/n each way per rank and step
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import xgmi_counters as XC
+    bus = torch.cuda.get_device_properties(dev).pci_bus_id
+    xg = None
+    c0 = XC.read(bus)
+    if c0 is not None:
+        reps = max(args.steps, 10)
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        xs = torch.rand(S // 4, device=dev, generator=g)
+        xr = torch.empty_like(xs)
+        dist.barrier()
+        for _ in range(reps):
+            MPI.Allreduce_(xs, xr, MPI.SUM, comm)
+        torch.cuda.synchronize()
+        dist.barrier()
+        time.sleep(0.2)  # let the metrics table refresh
+        c1 = XC.read(bus)
+        if c1 is not None:
+            rd = sum(b - a for a, b in zip(c0["read_kb"], c1["read_kb"])) * 1024 / reps
+            wr = sum(b - a for a, b in zip(c0["write_kb"], c1["write_kb"])) * 1024 / reps
+            algo_x = 2 * S * (n - 1) / n
+            xg = {"read_bytes_per_step": rd, "write_bytes_per_step": wr, "algorithmic_bytes_per_step": algo_x,
+                  "read_over_algorithmic": round(rd / algo_x, 4), "source": "amd-smi gpu_metrics xgmi_*_data_acc",
+                  "steps": reps}
+        del xs, xr
+
     # correctness on the timed path: SUM of rank-constant data is exact in f32
     chk = torch.full((1 << 20,), float(rank + 1), device=dev)
     out = torch.empty_like(chk)
@@ -438,7 +467,8 @@ def bench_allreduce(args):
                        "parallelism": f"{n} ranks x 1 GPU (hipIpc peer-mapped HBM over xGMI)",
                        "bytes_per_rank": S, "algbw_GBps": round(S / t / 1e9, 2)},
             "roofline": {"bound": "xgmi", "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
-                         "frac": round(ach / peak, 4), "traffic": None,
+                         "frac": round(ach / peak, 4),
+                         "traffic": xg["read_bytes_per_step"] if xg else None, "xgmi_traffic": xg,
                          "peak_basis": "measured: every rank pulling from all peers at once (mpigx_comm_probe)"
                                        if peak_meas else f"nominal {n - 1} x {XGMI_LINK_GBPS} GB/s",
                          "peak_nominal": peak_nom},
