@@ -355,6 +355,19 @@ def bench_allreduce(args):
             tw, _ = time_ar(nb, 10, 2)
             sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
         os.environ.pop("MPIGX_ALGO", None)
+    # push two-shot (remote stores into the peers' arenas / recvbufs) vs the
+    # default pull two-shot, with its own exactness check
+    os.environ["MPIGX_ALGO"] = "push"
+    for nb in (16 << 20, S, 1 << 30):
+        tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
+        sweep[f"{nb >> 20}MiB_push"] = round(busbw(nb, tw), 1)
+    big = torch.full((S // 4,), float(rank + 1), device=dev)
+    bout = torch.empty_like(big)
+    MPI.Allreduce_(big, bout, MPI.SUM, comm)
+    (bad,) = tmax(0.0 if bool(torch.all(bout == n * (n + 1) / 2).item()) else 1.0)
+    sweep["push_correct"] = bad == 0.0
+    del big, bout
+    os.environ.pop("MPIGX_ALGO", None)
     if args.no_rccl:
         rccl = {"skipped": True}
     else:

@@ -44,6 +44,9 @@ enum FoldMode : int {
   M_AR_ZC = 5,        // zero-copy two-shot: barrier, RS straight from the peers' (IPC-
                       // registered) send buffers into my recvbuf, barrier, AG from the
                       // peers' recvbufs, barrier
+  M_AR_PUSH = 6,      // push two-shot: write my chunk p into rank p's arena slot [me],
+                      // barrier, fold my chunk from my own slots (local HBM), write the
+                      // result into every rank's recvbuf (IPC-mapped), barrier
 };
 
 // Copy-kernel modes (Bcast / Allgather / Alltoall / Barrier).
@@ -95,7 +98,8 @@ struct FoldArgs {
   const void* src2[kMaxRanks];
   const void* send;    // collective modes: my send buffer (may be == recv)
   void* recv;          // output
-  char* zc_recv[kMaxRanks];  // M_AR_ZC: every rank's recvbuf (IPC-mapped; mine = recv)
+  char* zc_recv[kMaxRanks];  // M_AR_ZC / M_AR_PUSH: every rank's recvbuf (IPC-mapped; mine = recv)
+  long long slot_bytes;      // M_AR_PUSH: arena bytes per source slot (chunk bytes, 16-B multiple)
 };
 
 struct CopyArgs {

@@ -115,6 +115,63 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     return;
   }
 
+  if (A.mode == M_AR_PUSH) {
+    // push two-shot (the fold sources src[]/src2[] are my own arena slots and
+    // my sendbuf, resolved on the host).  No entry barrier: phase 1 writes
+    // only into the peers' arenas, which their previous launch (ended by a
+    // barrier of every block) no longer reads; their recvbufs are written
+    // only after barrier 1, i.e. after every rank entered this launch.
+    const int n = pv.n, r = pv.rank;
+    char* dsts[NMAX];
+    const char* srcs[NMAX];
+    long long lens[NMAX];
+    // phase 1: slice b of my chunk p -> rank p's slot [r], all peers at once
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      dsts[j] = nullptr;
+      srcs[j] = nullptr;
+      lens[j] = 0;
+      if (j + 1 < n) {
+        const int p = (r + 1 + j) % n;
+        const long long d0 = lmin((long long)p * A.chunk, A.count), d1 = lmin(d0 + A.chunk, A.count);
+        const long long l2 = lmin(d0 + (long long)b * A.slice, d1), h2 = lmin(l2 + A.slice, d1);
+        dsts[j] = pv.stage[p] + (long long)r * A.slot_bytes + (l2 - d0) * es;
+        srcs[j] = send + l2 * es;
+        lens[j] = (h2 - l2) * es;
+      }
+    }
+    block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    if (!rank_barrier(pv, ep++)) return;
+    // phase 2: fold my chunk (slots = local HBM) into my recvbuf, then write
+    // the reduced slice into every peer's recvbuf
+    const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+    bool vec = recv_vec;
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s)
+      if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
+#pragma unroll
+    for (int s = 0; s < NMAX / 2; ++s)
+      if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
+    fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      dsts[j] = nullptr;
+      srcs[j] = nullptr;
+      lens[j] = 0;
+      if (j + 1 < n) {
+        const int p = (r + 1 + j) % n;
+        dsts[j] = A.zc_recv[p] + lo * es;
+        srcs[j] = (const char*)(recv + lo);
+        lens[j] = (hi - lo) * es;
+      }
+    }
+    block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    rank_barrier(pv, ep++);  // every slice of my recvbuf has arrived
+    return;
+  }
+
   if (A.mode == M_AR_ONESHOT || A.mode == M_RED_ONESHOT) {
     const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
     block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);

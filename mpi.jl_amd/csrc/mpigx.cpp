@@ -451,6 +451,49 @@ int allreduce_zc(mpigx_comm* c, const char* const* psend, char* const* precv, lo
   return finish(c);
 }
 
+// Push two-shot Allreduce (MPIGX_ALGO=push; needs the zero-copy mapping of
+// every rank's recvbuf).  Rounds of at most n slots of one chunk each fit the
+// arena; per round: my chunk p -> rank p's slot [me] (remote stores), barrier,
+// fold my chunk from my slots + my sendbuf (same schedule as every other
+// path, so the same bits), result -> every rank's recvbuf, barrier.
+int allreduce_push(mpigx_comm* c, const void* send, char* const* precv, long long count, const TypeInfo* t,
+                   int oc) {
+  const int n = c->n, r = c->rank, es = t->size;
+  const int vec = es >= 16 ? 1 : 16 / es;
+  long long round = (long long)(c->stage_bytes / es);
+  round = (round / (n * (long long)vec)) * n * vec;
+  for (long long off = 0; off < count; off += round) {
+    const long long cnt = count - off < round ? count - off : round;
+    FoldArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.mode = M_AR_PUSH;
+    a.esize = es;
+    a.count = cnt;
+    a.gbase = off;
+    a.send = (const char*)send + off * es;
+    a.recv = precv[r] + off * es;
+    for (int p = 0; p < n; ++p) a.zc_recv[p] = precv[p] + off * es;
+    a.chunk = rup(cdiv(cnt, n), vec);
+    a.slot_bytes = a.chunk * es;
+    // leaf q of my chunk: slot q of my arena holds rank q's copy of it
+    // (indexed by the round-relative element e: slot base - c0), my own
+    // contribution is read straight from my sendbuf
+    const long long c0 = (long long)r * a.chunk;
+    const void* ptrs[kMaxRanks];
+    for (int q = 0; q < n; ++q)
+      ptrs[q] = q == r ? (const void*)a.send : (const void*)(c->stage + (long long)q * a.slot_bytes - c0 * es);
+    int nmax, sched;
+    plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
+    const int grid = grid_for(c, a.chunk * es);
+    a.slice = rup(cdiv(a.chunk, grid), vec);
+    HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
+    note_launch(c, a.pv, grid);
+    c->epoch += 2;
+  }
+  return finish(c);
+}
+
 // Shared driver for Allreduce / Reduce.
 int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, const TypeInfo* t,
                   int oc, int root, bool all) {
@@ -468,6 +511,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     char* pr[kMaxRanks];
     const int z = zc_resolve(c, send, recv, ps, pr);
     if (z < 0) return -z;
+    if (z == 1 && algo_env && !strcmp(algo_env, "push")) return allreduce_push(c, send, pr, count, t, oc);
     if (z == 1) return allreduce_zc(c, ps, pr, count, t, oc);
     if (c->zc_require) return MPIGX_ERR_INTERN;  // tests: the path must not fall back
   }

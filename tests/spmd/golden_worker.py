@@ -25,6 +25,9 @@ from golden_io import load, same_bits, typed  # noqa: E402
 from oracle import mpich_model as M  # noqa: E402
 
 IN_PLACE = ctypes.c_void_p(-1 & ((1 << 64) - 1))
+# Allreduce algorithms to run every case through; the push two-shot needs the
+# zero-copy mapping, so it joins when the zero-copy test forces that path
+AR_ALGOS = ("oneshot", "twoshot") + (("push",) if os.environ.get("MPIGX_ZC_MIN") else ())
 
 
 def dev(a):
@@ -117,7 +120,7 @@ class Runner:
             ins = typed(arr[c["id"] + ".in"], npdt)
             outs = typed(arr[c["id"] + ".out"], npdt)
             coll = c["coll"]
-            algos = ("oneshot", "twoshot") if coll in ("allreduce", "reduce") else ("auto",)
+            algos = AR_ALGOS if coll in ("allreduce", "reduce") else ("auto",)
             for algo in algos:
                 os.environ["MPIGX_ALGO"] = algo
                 for inplace in (False, True):
@@ -227,7 +230,7 @@ class Runner:
         n, r = self.n, self.r
         for i, (dtname, opname, count) in enumerate(sizes):
             ins = make(dtname, opname, n, count, 1000 + i, edge=opname in ("MAX", "MIN"))
-            for algo in ("oneshot", "twoshot"):
+            for algo in AR_ALGOS:
                 os.environ["MPIGX_ALGO"] = algo
                 got = self.run("allreduce", ins, dtname, opname, count)
                 self.check(same_bits(got, M.allreduce(ins, dtname, opname)[r], dtname == "BFLOAT16"), ("oracle-allreduce", dtname, opname, count, algo))
@@ -266,7 +269,7 @@ class Runner:
         for i, (dtname, opname, count) in enumerate((("FLOAT", "SUM", 5000), ("DOUBLE", "SUM", 70001),
                                                     ("FLOAT", "MAX", 3000), ("BFLOAT16", "SUM", 9999))):
             ins = make(dtname, opname, self.n, count, 500 + i, edge=opname == "MAX")
-            for algo in ("oneshot", "twoshot"):
+            for algo in AR_ALGOS:
                 os.environ["MPIGX_ALGO"] = algo
                 got = self.run("allreduce", ins, dtname, opname, count)
                 self.check(same_bits(got, M.fold_linear(ins, dtname, opname), dtname == "BFLOAT16"), ("linear", dtname, opname, algo))

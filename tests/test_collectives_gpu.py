@@ -28,10 +28,11 @@ def test_golden_collectives(n):
     print(summ[0])
 
 
-@pytest.mark.parametrize("n", [2, 3, 5])
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
 def test_golden_collectives_zero_copy(n):
-    """Every Allreduce through the zero-copy path (peers read the user buffers
-    through cached hipIpc registrations; MPIGX_ZC_MIN=1 forces it at every size)."""
+    """Every Allreduce through the zero-copy paths (pull: peers read the user
+    buffers through cached hipIpc registrations; push: ranks write into the
+    peers' arenas and recvbufs); MPIGX_ZC_MIN=1 forces them at every size."""
     env = dict(ENV, MPIGX_ZC_MIN="1", MPIGX_ZC_REQUIRE="1")
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "golden_worker.py"), n, timeout=900, extra_env=env)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
