@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--cpu-iters", type=int, default=30)
     p.add_argument("--no-rccl", action="store_true", help="skip the RCCL comparison (N>1)")
     p.add_argument("--no-extra", action="store_true", help="skip the config-4/5 blocks (N>1)")
+    p.add_argument("--no-sweep", action="store_true",
+                   help="N=1: skip the size sweep (rocprof runs, so the headline kernel's stats hold 256 MiB launches only)")
     return p.parse_args()
 
 
@@ -201,7 +203,7 @@ def bench_local(args):
 
     # message-size sweep of the same kernel (f32 SUM, 8 inputs), kernel time
     sweep = {}
-    for mib in (1, 4, 16, 64):
+    for mib in (() if args.no_sweep else (1, 4, 16, 64)):
         k = mib << 18
         xs = [x[:k] for x in ins]
         o = out[:k]

@@ -12,9 +12,9 @@ OUT=$R/gpurun_out/prof_$TAG
 rm -rf "$OUT"; mkdir -p "$OUT"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$R/bench.py" --no-cpu-baseline --steps 10 "$@" > "$OUT/trace.log" 2>&1
+  python3 "$R/bench.py" --no-cpu-baseline --no-sweep --steps 10 "$@" > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- \
-  python3 "$R/bench.py" --no-cpu-baseline --steps 5 --warmup 1 "$@" > "$OUT/fetch.log" 2>&1
+  python3 "$R/bench.py" --no-cpu-baseline --no-sweep --steps 5 --warmup 1 "$@" > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- \
-  python3 "$R/bench.py" --no-cpu-baseline --steps 5 --warmup 1 "$@" > "$OUT/write.log" 2>&1
+  python3 "$R/bench.py" --no-cpu-baseline --no-sweep --steps 5 --warmup 1 "$@" > "$OUT/write.log" 2>&1
 python3 "$R/tools/summarize_prof.py" "$OUT" "$R/profiles" "$TAG"
