@@ -56,7 +56,8 @@ enum FoldMode : int {
 //                 xGMI link carries <= 2S/n instead of each root link carrying S
 enum CopyMode : int {
   C_BCAST = 0, C_ALLGATHER = 1, C_ALLTOALL = 2, C_BARRIER = 3, C_PROBE_ALL = 4, C_PROBE_ONE = 5,
-  C_BCAST_SAG = 6
+  C_BCAST_SAG = 6,
+  C_ALLTOALL_ZC = 7  // zero-copy: pull block r straight from every rank's (IPC-mapped) sendbuf
 };
 
 // Per-call view of the communicator, passed by value to every kernel.
@@ -111,6 +112,7 @@ struct CopyArgs {
   long long total;     // user-buffer stride between rank blocks (bytes of one full block)
   long long sstride;   // alltoall: staging stride between rank blocks (bytes rounded up to 16)
   long long chunk;     // bcast-sag: bytes per rank chunk (multiple of 16)
+  const char* zsrc[kMaxRanks];  // alltoall-zc: every rank's sendbuf (IPC-mapped; mine = send)
   const void* send;
   void* recv;
 };

@@ -128,6 +128,27 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
     rank_barrier(pv, ep++);
     return;
   }
+  if (A.mode == C_ALLTOALL_ZC) {
+    // no staging: block r of rank p's sendbuf -> block p of my recvbuf
+    if (!rank_barrier(pv, ep++)) return;  // every rank's sendbuf is ready
+    int m = 0;
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      dsts[j] = nullptr;
+      srcs[j] = nullptr;
+      lens[j] = 0;
+      if (j < n) {
+        const int p = (r + j) % n;
+        dsts[j] = recv + (long long)p * A.total + lo;
+        srcs[j] = A.zsrc[p] + (long long)r * A.total + lo;
+        lens[j] = len;
+        m = j + 1;
+      }
+    }
+    block_gather<NMAX>(dsts, srcs, lens, m);
+    rank_barrier(pv, ep++);  // nobody reads my sendbuf any more
+    return;
+  }
   // C_ALLTOALL: block p of my send goes to rank p; block j of my recv comes
   // from rank j's block r.  Staging blocks are A.sstride (16-B multiple) apart.
   for (int p = 0; p < n; ++p) block_copy(mine + (long long)p * A.sstride + lo, send + (long long)p * A.total + lo, len);

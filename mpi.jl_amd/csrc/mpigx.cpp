@@ -1171,6 +1171,33 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
   const char* s = inplace ? (alltoall ? (const char*)recv : (const char*)recv + (long long)r * bytes)
                           : (const char*)send;
   if (n == 1) return copy_n1(c, alltoall ? recv : (char*)recv, s, bytes);
+  // large out-of-place Alltoall: pull straight from the peers' sendbufs (no
+  // copy-in, no rounds).  IN_PLACE is given by every rank or none (MPI), and
+  // (bytes, n, thresholds) agree, so every rank takes the same branch.
+  if (alltoall && !inplace && c->zc_min > 0 && bytes * n >= c->zc_min) {
+    const char* ps[kMaxRanks];
+    char* pr[kMaxRanks];
+    const int z = zc_resolve(c, s, recv, ps, pr);
+    if (z < 0) return -z;
+    if (z == 1) {
+      CopyArgs a;
+      memset(&a, 0, sizeof a);
+      a.pv = make_view(c);
+      a.mode = C_ALLTOALL_ZC;
+      a.bytes = bytes;
+      a.total = bytes;
+      for (int p = 0; p < n; ++p) a.zsrc[p] = ps[p];
+      const int g = grid_for(c, bytes * n);
+      a.slice = rup(cdiv(bytes, g), 16);
+      a.send = s;
+      a.recv = recv;
+      HIPCK(launch_copy(dim3(g), c->stream, a));
+      note_launch(c, a.pv, g);
+      c->epoch += 2;
+      return finish(c);
+    }
+    if (c->zc_require) return MPIGX_ERR_INTERN;
+  }
   // rounds: allgather stages `bytes` per rank; alltoall stages n*round
   const long long cap = alltoall ? (long long)(c->stage_bytes / n) & ~15ll : (long long)c->stage_bytes & ~15ll;
   for (long long off = 0; off < bytes; off += cap) {
