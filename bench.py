@@ -235,7 +235,7 @@ def bench_local(args):
                    "algorithmic_bytes_per_step": algo},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": "fold_kernel<OpSum,float,8,TREE> (M_LOCAL)", "kernel_ms": round(kern_ms, 4)},
+                     "kernel": "fold_local_kernel<OpSum,float,8,TREE>", "kernel_ms": round(kern_ms, 4)},
         "cpu_baseline": cpu,
         "parity_sample_bit_exact": parity,
         "hbm_copy_peak_GBps_measured": round(copy_gbps, 1),

@@ -48,6 +48,27 @@ __global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
   signal_done(A.pv);
 }
 
+// Config-2 local multi-buffer reduce in a kernel of its own: the collective
+// modes index FoldArgs with per-rank values, which for the role-sensitive
+// ops (float MIN/MAX) made the compiler copy the whole 840-B argument block
+// to scratch in every thread at entry — 16 M threads x 840 B per 256 MiB
+// call held f32 MAX at 0.67 TB/s.  This kernel touches only M_LOCAL fields.
+template <class OP, class T, int NMAX, int SCHED>
+__global__ __launch_bounds__(kThreads) void fold_local_kernel(FoldArgs A) {
+  const T* const* src = reinterpret_cast<const T* const*>(A.src);
+  const T* const* src2 = reinterpret_cast<const T* const*>(A.src2);
+  bool vec = ((uintptr_t)A.recv & 15) == 0;
+#pragma unroll
+  for (int s = 0; s < NMAX; ++s)
+    if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
+#pragma unroll
+  for (int s = 0; s < NMAX / 2; ++s)
+    if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
+  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x,
+                  gnt = (long long)gridDim.x * blockDim.x;
+  fold_range<OP, T, NMAX, SCHED>(A, src, src2, 0, A.count, (T*)A.recv, nullptr, vec, gtid, gnt);
+}
+
 template <class OP, class T, int NMAX, int SCHED>
 __device__ __forceinline__ void fold_body(const FoldArgs& A) {
   const T* const* src = reinterpret_cast<const T* const*>(A.src);
