@@ -21,12 +21,16 @@ constexpr bool kCplx = is_cplx<T>::v;
 template <class OP>
 hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a) {
   if (a.mode == M_LOCAL) {
-    if (sched == S_LINEAR)
+    if (sched == S_LINEAR && nmax <= 8)
+      hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_LINEAR>), grid, dim3(kThreads), 0, s, a);
+    else if (sched == S_LINEAR)
       hipLaunchKernelGGL((fold_local_kernel<OP, T, 16, S_LINEAR>), grid, dim3(kThreads), 0, s, a);
     else if (nmax <= 8)
       hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_TREE>), grid, dim3(kThreads), 0, s, a);
     else
       hipLaunchKernelGGL((fold_local_kernel<OP, T, 16, S_TREE>), grid, dim3(kThreads), 0, s, a);
+  } else if (sched == S_LINEAR && nmax <= 8) {
+    hipLaunchKernelGGL((fold_kernel<OP, T, 8, S_LINEAR>), grid, dim3(kThreads), 0, s, a);
   } else if (sched == S_LINEAR) {
     hipLaunchKernelGGL((fold_kernel<OP, T, 16, S_LINEAR>), grid, dim3(kThreads), 0, s, a);
   } else if (nmax <= 8) {

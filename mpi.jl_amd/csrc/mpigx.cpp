@@ -277,7 +277,7 @@ void plan_schedule(mpigx_comm* c, FoldArgs& a, int n, int root, long long count_
   (void)c;
   if (order == MPIGX_ORDER_LINEAR) {
     *sched = S_LINEAR;
-    *nmax = 16;
+    *nmax = n <= 8 ? 8 : 16;  // NMAX 16 kernels carry an 840-B scratch entry copy
     a.ntree = n;
     for (int k = 0; k < n; ++k) a.src[k] = ptrs[k];
     return;
