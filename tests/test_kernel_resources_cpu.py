@@ -1,0 +1,55 @@
+"""Scratch (private segment) guard for the hot kernels, read from the built
+gfx950 code objects' metadata — no GPU needed.
+
+A kernel that lands in scratch runs an order of magnitude slower on a
+one-vector-per-thread grid: the all-modes fold_kernel for float MAX copied
+its 840-B FoldArgs to scratch per thread and ran config 2 at 0.67 TB/s
+(DESIGN.md §5).  This pins the fix: every fold_local_kernel (config 2) and
+every NMAX-8 SUM fold_kernel (the headline Allreduce at <= 8 ranks) has a
+zero private segment.
+"""
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, "mpi.jl_amd", "build")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _kernel_private_sizes(obj, tmp):
+    fb, co = os.path.join(tmp, "fb.bin"), os.path.join(tmp, "co.elf")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", obj, os.devnull], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
+                           capture_output=True, text=True).stdout
+    sizes, name = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s*\.name:\s+(\S+)", line)
+        if m:
+            name = m.group(1)
+            continue
+        m = re.match(r"\s*\.private_segment_fixed_size:\s+(\d+)", line)
+        if m and name:
+            sizes[name] = int(m.group(1))
+    return sizes
+
+
+OBJS = sorted(glob.glob(os.path.join(BUILD, "kern_*.o")))
+
+
+@pytest.mark.skipif(not OBJS or not os.path.exists(f"{LLVM}/clang-offload-bundler"),
+                    reason="kernel objects not built (run __graft_entry__.build())")
+@pytest.mark.parametrize("obj", OBJS, ids=[os.path.basename(o) for o in OBJS])
+def test_hot_fold_kernels_have_no_scratch(obj, tmp_path):
+    sizes = _kernel_private_sizes(obj, str(tmp_path))
+    local = {k: v for k, v in sizes.items() if "fold_local_kernel" in k}
+    assert local, f"no fold_local_kernel in {obj}"
+    assert all(v == 0 for v in local.values()), {k: v for k, v in local.items() if v}
+    sum8 = {k: v for k, v in sizes.items() if re.search(r"11fold_kernelINS_5OpSumE.*Li8ELi", k)}
+    assert sum8, f"no NMAX-8 SUM fold_kernel in {obj}"
+    assert all(v == 0 for v in sum8.values()), {k: v for k, v in sum8.items() if v}
