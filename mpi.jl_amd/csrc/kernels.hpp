@@ -44,8 +44,24 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A);
 
 template <class OP, class T, int NMAX, int SCHED>
 __global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
-  fold_body<OP, T, NMAX, SCHED>(A);
-  signal_done(A.pv);
+  // The collective modes index FoldArgs with per-rank values.  For float
+  // MIN/MAX and the NMAX-16 kernels the compiler then copied the whole
+  // 840-B argument block to per-thread scratch at entry; those kernels stage
+  // it once per block in LDS instead.  The others (the SUM/NMAX-8 headline
+  // among them) keep reading it from the kernarg segment with scalar loads.
+  if constexpr (NMAX > 8 || role_sensitive<OP, T>::v) {
+    __shared__ FoldArgs sA;
+    static_assert(sizeof(FoldArgs) % 4 == 0, "FoldArgs word copy");
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&A);
+    uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
+    for (unsigned i = threadIdx.x; i < sizeof(FoldArgs) / 4; i += blockDim.x) d[i] = w[i];
+    __syncthreads();
+    fold_body<OP, T, NMAX, SCHED>(sA);
+    signal_done(sA.pv);
+  } else {
+    fold_body<OP, T, NMAX, SCHED>(A);
+    signal_done(A.pv);
+  }
 }
 
 // Config-2 local multi-buffer reduce in a kernel of its own: the collective
