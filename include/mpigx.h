@@ -131,10 +131,17 @@ int mpigx_comm_device(mpigx_comm_t comm, int *device);
  * the null stream. */
 int mpigx_comm_set_stream(mpigx_comm_t comm, void *stream);
 /* 1 (default): every call returns with results complete.  0: calls only
- * enqueue on the stream (RCCL-like); mpigx_comm_synchronize reports errors. */
+ * enqueue on the stream (RCCL-like); mpigx_comm_synchronize reports errors.
+ * Every rank of a communicator must use the same mode (the zero-copy
+ * protocol differs between the two). */
 int mpigx_comm_set_blocking(mpigx_comm_t comm, int blocking);
 int mpigx_comm_synchronize(mpigx_comm_t comm);
 int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
+/* Zero-copy paths (user buffers mapped by the peers over IPC): how many
+ * launches ran on a cached view without any host exchange, and how many
+ * host exchanges of buffer registrations there were.  Diagnostic. */
+int mpigx_comm_zc_stats(mpigx_comm_t comm, unsigned long long *optimistic_hits,
+                        unsigned long long *exchanges);
 
 /* Diagnostic (bench roofline denominator): every rank pulls `bytes` from
  * every peer's staging arena at once (kind 0: aggregate xGMI ingress) or
@@ -351,7 +358,9 @@ int mpigx_get_accumulate(const void *origin_addr, int origin_count, int origin_d
 
 /* ---- derived datatypes (src/datatypes.jl:62-318) ---
  * The MPI_Type_* constructors MPI.Types ccalls, for device buffers: handles
- * are `int`s in MPICH's derived-type space (0x8c000000 | index), usable
+ * are `int`s in libmpigx's own space (0x3d000000 | generation << 16 | slot,
+ * never issued by MPICH: an MPICH derived type is rejected with
+ * MPI_ERR_TYPE, not aliased), usable
  * wherever a datatype is taken once committed — point-to-point (strided and
  * dense SubArrays, buffers.jl:104-117; padded isbits structs,
  * datatypes.jl:269-316) and the byte-moving collectives (Bcast, Allgather,
@@ -384,9 +393,12 @@ int mpigx_unpack(const void *inbuf, long long insize, long long *position, void 
                  int datatype, void *stream);
 
 /* ---- user-defined ops (operators.jl:56-88 OpWrapper) --
- * MPI_Op_create analogues.  Handles live in MPICH's user-op space
- * (0x98000000 | index) and are accepted by Allreduce / Reduce / Scan /
- * Exscan for predefined and contiguous derived types.  The engine gathers
+ * MPI_Op_create analogues.  Handles live in libmpigx's own space
+ * (0x3c000000 | generation << 16 | slot: MPICH never issues a kind-00 handle
+ * with a non-zero payload), so an op MPI.jl created in libmpi (MPICH user op
+ * 0x98000000 | k) is rejected with MPI_ERR_OP instead of aliasing one of
+ * these; a freed handle is rejected too.  Accepted by Allreduce / Reduce /
+ * Scan / Exscan for predefined and contiguous derived types.  The engine gathers
  * the contributions with its own kernels and folds in rank order,
  * inout = x_q (op) inout from the highest contributing rank down.
  *   host callback   — MPI_User_function on HOST copies (what MPI.jl's

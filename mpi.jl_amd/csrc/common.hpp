@@ -31,6 +31,23 @@ enum OpCode : int {
 constexpr int O_REPLACE = 16;
 constexpr int O_NOOP = 17;
 
+// Fold shapes (template parameter of the fold code): SH_PRE — pre-step
+// partners possible (n not a power of two); SH_POW2 — none; SH_FULL — none
+// and every one of the NMAX leaves present (no runtime guards at all).
+enum Shape : int { SH_PRE = 0, SH_POW2 = 1, SH_FULL = 2 };
+
+// The local fold's shape and 16-B vectors per thread — ONE rule for the host
+// (grid size) and the launcher (instantiation).  SH_FULL only at NMAX 8 (the
+// 8-buffer headline; n = 16 takes SH_POW2).  U = 4 measured best or tied on
+// three MI355X boxes (tools/fold_tune.hip, profiles/r02_fold_tune*.json);
+// bf16 MIN/MAX keep U = 1 (their owner-dispatched trees need the VGPRs).
+constexpr int fold_shape(int sched, int nmax, int ntree, int rem) {
+  return (sched == 0 && rem > 0) ? SH_PRE : (nmax == 8 && ntree == 8) ? SH_FULL : SH_POW2;
+}
+constexpr int local_u(int rep, int op, int shape) {
+  return shape != SH_FULL ? 1 : (rep == R_BF16 && (op == O_MIN || op == O_MAX)) ? 1 : 4;
+}
+
 // Fold schedule (template parameter of the fold kernels).
 enum Sched : int { S_TREE = 0, S_LINEAR = 1 };
 
@@ -73,6 +90,10 @@ struct PeerView {
   unsigned long long dbase;    // dcount value before this launch
   unsigned long long seq;      // value the last block of this launch stores to *done
   char* stage[kMaxRanks];      // staging arena base of every rank (IPC-mapped)
+  // zero-copy launches (mpigx.cpp zc_run)
+  unsigned zc_key;             // id of the buffer-mapping view this launch uses
+  int zc_bad;                  // 1: this rank has no valid view (the launch aborts everywhere)
+  unsigned* zc_stale;          // host-visible: set when a zero-copy launch aborted
 };
 
 // Fold-kernel arguments.  Sources/partition are resolved on the host.
@@ -90,6 +111,7 @@ struct FoldArgs {
   int owner_mode;      // 0: lower subtree is inout (binomial); 1: Rabenseifner owner roles
   int pof2_log;        // log2(pof2) for owner computation
   long long blk_len;   // Rabenseifner block length (count_total / pof2)
+  double blk_inv;      // 1.0 / blk_len (owner_block: reciprocal + one-step fix-up)
   int root;            // reduce root (rank)
   // leaf -> rank maps for collective modes (staging-sourced)
   signed char leaf_rank[kMaxRanks];

@@ -130,7 +130,9 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
   }
   if (A.mode == C_ALLTOALL_ZC) {
     // no staging: block r of rank p's sendbuf -> block p of my recvbuf
-    if (!rank_barrier(pv, ep++)) return;  // every rank's sendbuf is ready
+    int ab;
+    if (!zc_enter(pv, ep++, &ab)) return;  // every rank's sendbuf is ready
+    if (!ab) {
     int m = 0;
 #pragma unroll
     for (int j = 0; j < NMAX; ++j) {
@@ -146,7 +148,9 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
       }
     }
     block_gather<NMAX>(dsts, srcs, lens, m);
-    rank_barrier(pv, ep++);  // nobody reads my sendbuf any more
+    }
+    rank_barrier(pv, ep++, &ab);  // nobody reads my sendbuf any more
+    zc_leave(pv, ab);
     return;
   }
   // C_ALLTOALL: block p of my send goes to rank p; block j of my recv comes

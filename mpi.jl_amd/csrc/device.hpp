@@ -172,6 +172,51 @@ template <class OP, class T> struct role_sensitive {
   static constexpr bool v = is_real_fp<T>::v && (OP::code == O_MIN || OP::code == O_MAX);
 };
 
+// ---------------------------------------------------------------------------
+// bf16 pairs: two bf16 in one dword, the ops on both at once.  The same
+// definition as OpSum/OpProd/OpMax/OpMin::apply on bf16 (fp32 compute, RNE to
+// bf16 after the op, NaN kept quiet with its sign and top payload), in fewer
+// instructions: one v_pk_add_f32 / v_pk_mul_f32 and one v_cvt_pk_bf16_f32 per
+// pair instead of 2 x (add + software RNE + repack); MIN/MAX select whole
+// dwords and merge the halves with one bitfield insert.  gfx950's
+// v_cvt_pk_bf16_f32 rounds to nearest even and turns a NaN into
+// (bits >> 16) | 0x40 — the software f2bf above (MPIGX_HW_BF16=0 builds that
+// instead; tests/test_local_gpu.py checks random bit patterns against the oracle).
+// ---------------------------------------------------------------------------
+#ifndef MPIGX_HW_BF16
+#define MPIGX_HW_BF16 1
+#endif
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2_t bf16x2_to_f32x2(uint32_t a) {
+  return f32x2_t{__uint_as_float(a << 16), __uint_as_float(a & 0xffff0000u)};
+}
+__device__ __forceinline__ uint32_t f32x2_to_bf16x2(f32x2_t f) {
+#if MPIGX_HW_BF16
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
+#else
+  return (uint32_t)f2bf(f.x).u | ((uint32_t)f2bf(f.y).u << 16);
+#endif
+}
+
+template <class OP>
+__device__ __forceinline__ uint32_t bf16x2_apply(uint32_t a, uint32_t b) {  // a = inout, b = in
+  if constexpr (OP::code == O_SUM) {
+    return f32x2_to_bf16x2(bf16x2_to_f32x2(a) + bf16x2_to_f32x2(b));
+  } else if constexpr (OP::code == O_PROD) {
+    return f32x2_to_bf16x2(bf16x2_to_f32x2(a) * bf16x2_to_f32x2(b));
+  } else if constexpr (OP::code == O_MAX || OP::code == O_MIN) {
+    const f32x2_t fa = bf16x2_to_f32x2(a), fb = bf16x2_to_f32x2(b);
+    const bool lo = OP::code == O_MAX ? fa.x > fb.x : fa.x < fb.x;
+    const bool hi = OP::code == O_MAX ? fa.y > fb.y : fa.y < fb.y;
+    return ((lo ? a : b) & 0xffffu) | ((hi ? a : b) & 0xffff0000u);
+  } else {
+    bf16 x0{(uint16_t)a}, x1{(uint16_t)(a >> 16)}, y0{(uint16_t)b}, y1{(uint16_t)(b >> 16)};
+    return (uint32_t)OP::apply(x0, y0).u | ((uint32_t)OP::apply(x1, y1).u << 16);
+  }
+}
+
 // 16-byte register vector for the streaming paths
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef MPIGX_NT
@@ -219,6 +264,59 @@ __device__ __forceinline__ void st(T* p, const T (&d)[W]) {
   }
 }
 
+// Register vector of W elements of T for the fold / scan arithmetic.  bf16
+// vectors live as packed dword pairs — the form a 16-B load delivers and the
+// pair ops (bf16x2_apply) consume — so no 16-bit element ever occupies a
+// register of its own (an array of bf16 structs was split into eight 16-bit
+// values per vector: twice the VGPRs plus unpack / repack instructions).
+template <class T, int W>
+struct Vec {
+  static constexpr bool packed = std::is_same<T, bf16>::value && W % 2 == 0;
+  using S = typename std::conditional<packed, uint32_t, T>::type;
+  static constexpr int N = packed ? W / 2 : W;
+  S x[N];
+  __device__ __forceinline__ T at(int w) const {
+    if constexpr (packed) return bf16{(uint16_t)(x[w / 2] >> (16 * (w & 1)))};
+    else return x[w];
+  }
+};
+
+template <class T, int W>
+__device__ __forceinline__ void ldv(Vec<T, W>& d, const T* p) {
+  if constexpr (W * sizeof(T) == 16) {
+    *reinterpret_cast<u32x4*>(d.x) = ld16(p);
+  } else {
+    static_assert(!Vec<T, W>::packed, "packed vectors are 16 B");
+#pragma unroll
+    for (int w = 0; w < W; ++w) d.x[w] = p[w];
+  }
+}
+template <class T, int W>
+__device__ __forceinline__ void stv(T* p, const Vec<T, W>& d) {
+  if constexpr (W * sizeof(T) == 16) {
+    st16(p, *reinterpret_cast<const u32x4*>(d.x));
+  } else {
+#pragma unroll
+    for (int w = 0; w < W; ++w) p[w] = d.x[w];
+  }
+}
+
+// d = OP(a, b) element-wise, a = inout (d may alias a or b)
+template <class OP, class T, int W>
+__device__ __forceinline__ void vapply(Vec<T, W>& d, const Vec<T, W>& a, const Vec<T, W>& b) {
+  using V = Vec<T, W>;
+  typename V::S t[V::N];
+  if constexpr (V::packed) {
+#pragma unroll
+    for (int i = 0; i < V::N; ++i) t[i] = bf16x2_apply<OP>(a.x[i], b.x[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V::N; ++i) t[i] = OP::apply(a.x[i], b.x[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < V::N; ++i) d.x[i] = t[i];
+}
+
 // ---------------------------------------------------------------------------
 // fold of the leaves at element e (W consecutive elements)
 //   TREE  : pre-step (leaf s < rem: src[s] = OP(src[s], src2[s])), then the
@@ -230,82 +328,154 @@ __device__ __forceinline__ unsigned bitrev(unsigned j, int L) {
   return L == 0 ? 0u : (__builtin_bitreverse32(j) >> (32 - L));
 }
 
-template <class OP, class T, int NMAX, int SCHED, int W>
-__device__ __forceinline__ void fold_at(const FoldArgs& A, const T* const* src, const T* const* src2,
-                                        long long e, T (&res)[W]) {
-  T v[NMAX][W];
+// The leaves of W consecutive elements, loaded before any arithmetic so a
+// thread's loads (and with U > 1 several vectors' loads) are all in flight
+// together.  SHAPE (common.hpp): SH_PRE — pre-step partners possible (n not a
+// power of two; they exist only for s < rem <= NMAX/2); SH_POW2 — none;
+// SH_FULL — none and ntree == NMAX, so no leaf load or tree node carries a
+// runtime guard (the 8-buffer headline shape).
+template <class T, int NMAX, int SHAPE, int W>
+struct Leaves {
+  Vec<T, W> v[NMAX];
+  Vec<T, W> u[SHAPE == SH_PRE ? NMAX / 2 : 1];
+};
+
+template <int NMAX, int SHAPE>
+__device__ __forceinline__ int ntree_of(const FoldArgs& A) {
+  return SHAPE == SH_FULL ? NMAX : A.ntree;
+}
+
+template <class T, int NMAX, int SCHED, int SHAPE, int W>
+__device__ __forceinline__ void load_leaves(const FoldArgs& A, const T* const* src, const T* const* src2,
+                                            long long e, Leaves<T, NMAX, SHAPE, W>& L) {
+  const int nt = ntree_of<NMAX, SHAPE>(A);
 #pragma unroll
   for (int s = 0; s < NMAX; ++s)
-    if (s < A.ntree) ld<T, W>(v[s], src[s] + e);
-  if constexpr (SCHED == S_LINEAR) {
+    if (s < nt) ldv<T, W>(L.v[s], src[s] + e);
+  if constexpr (SHAPE == SH_PRE && SCHED == S_TREE) {
 #pragma unroll
-    for (int s = 1; s < NMAX; ++s)
-      if (s < A.ntree) {
+    for (int s = 0; s < NMAX / 2; ++s)
+      if (s < A.rem) ldv<T, W>(L.u[s], src2[s] + e);
+  }
+}
+
+// Pairwise tree over the leaves with MPICH's operand roles.  At level m the
+// node (s, s+m) takes as inout the subtree holding the element's owner
+// newrank (Rabenseifner: block j is finished on newrank bitrev(j); binomial:
+// the lower subtree, i.e. owner 0).  The owner is the same for all W
+// elements (fold_leaves guarantees it) and a compile-time constant here, so
+// every node is ONE op with fixed roles — no evaluation of both orders and no
+// selects; fold_tree_own dispatches the runtime owner (wave-uniform except at
+// the pof2-1 block boundaries) to the NMAX instantiations.
+template <class OP, class T, int NMAX, int W, int OWN>
+__device__ __forceinline__ void fold_tree(int ntree, Vec<T, W> (&v)[NMAX]) {
+  if constexpr (Vec<T, W>::packed && OWN > 0) {
+    // every owner instantiation starts by widening the same packed leaves;
+    // hoisted above fold_tree_own's dispatch, the widened copies of all
+    // leaves stay live at once (twice the VGPRs of the packed ones)
 #pragma unroll
-        for (int w = 0; w < W; ++w) v[0][w] = OP::apply(v[0][w], v[s][w]);
-      }
-  } else {
-    if (A.rem > 0) {
+    for (int s = 0; s < NMAX; ++s)
 #pragma unroll
-      for (int s = 0; s < NMAX / 2; ++s)
-        if (s < A.rem) {
-          T u[W];
-          ld<T, W>(u, src2[s] + e);
+      for (int i = 0; i < Vec<T, W>::N; ++i) asm volatile("" : "+v"(v[s].x[i]));
+  }
 #pragma unroll
-          for (int w = 0; w < W; ++w) v[s][w] = OP::apply(v[s][w], u[w]);
-        }
-    }
-    unsigned own[W];
+  for (int m = 1; m < NMAX; m <<= 1) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) own[w] = 0;
-    if constexpr (role_sensitive<OP, T>::v) {
-      if (A.owner_mode) {
-        // Rabenseifner block of each element: one 64-bit division per vector,
-        // then step across the (rare) block boundaries inside the vector
-        const unsigned pof2 = 1u << A.pof2_log;
-        const unsigned long long g0 = (unsigned long long)(A.gbase + e), bl = (unsigned long long)A.blk_len;
-        // no data-dependent loop here: a `while` inside the unrolled w loop
-        // kept it rolled and pushed v[][] to scratch (840 B/lane, f32 MAX
-        // at 0.67 TB/s).  bl >= W crosses at most one boundary per vector.
-        const unsigned long long j0 = g0 / bl, next = (j0 + 1) * bl;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          const unsigned long long j = bl >= (unsigned long long)W ? j0 + (g0 + w >= next ? 1ull : 0ull)
-                                                                  : (g0 + w) / bl;
-          own[w] = bitrev((unsigned)(j > pof2 - 1 ? pof2 - 1 : j), A.pof2_log);
-        }
-      }
-    }
-#pragma unroll
-    for (int m = 1; m < NMAX; m <<= 1) {
-#pragma unroll
-      for (int s = 0; s + m < NMAX; s += 2 * m) {
-        if (s + m < A.ntree) {
-#pragma unroll
-          for (int w = 0; w < W; ++w) {
-            if constexpr (role_sensitive<OP, T>::v) {
-              // operands are swapped by value: a select between the two
-              // array slots became a select of addresses and moved v[][]
-              // to scratch (840 B/lane)
-              const T lo = v[s][w], hi = v[s + m][w];
-              const T r0 = OP::apply(lo, hi), r1 = OP::apply(hi, lo);
-              v[s][w] = (own[w] & (unsigned)m) ? r1 : r0;
-            } else {
-              v[s][w] = OP::apply(v[s][w], v[s + m][w]);
-            }
-          }
-        }
+    for (int s = 0; s + m < NMAX; s += 2 * m) {
+      if (s + m < ntree) {
+        if ((OWN & m) != 0) vapply<OP, T, W>(v[s], v[s + m], v[s]);
+        else vapply<OP, T, W>(v[s], v[s], v[s + m]);
       }
     }
   }
+}
+
+// Rabenseifner block of element g: j = min(pof2-1, g / blk_len) from a double
+// reciprocal plus a one-step correction (no 64-bit division per vector).
+__device__ __forceinline__ unsigned owner_block(const FoldArgs& A, unsigned long long g) {
+  const unsigned long long bl = (unsigned long long)A.blk_len;
+  unsigned long long j = (unsigned long long)((double)g * A.blk_inv);
+  if (j * bl > g) --j;
+  else if ((j + 1) * bl <= g) ++j;
+  const unsigned long long top = (1ull << A.pof2_log) - 1;
+  return (unsigned)(j > top ? top : j);
+}
+
+template <class OP, class T, int NMAX, int W, int K>
+__device__ __forceinline__ void fold_tree_own(int own, int ntree, Vec<T, W> (&v)[NMAX]) {
+  if constexpr (K < NMAX) {
+    if (own == K) fold_tree<OP, T, NMAX, W, K>(ntree, v);
+    else fold_tree_own<OP, T, NMAX, W, K + 1>(own, ntree, v);
+  }
+}
+
+// Fold the loaded leaves of the W elements starting at e into res.  Returns
+// false, leaving res unset, when the W elements straddle a Rabenseifner block
+// boundary with role-sensitive operands (at most pof2-1 vectors per call):
+// the caller then folds those elements one at a time (fold_elems), so the
+// W-wide code only ever runs with one owner per vector.
+template <class OP, class T, int NMAX, int SCHED, int SHAPE, int W>
+__device__ __forceinline__ bool fold_leaves(const FoldArgs& A, long long e, Leaves<T, NMAX, SHAPE, W>& L,
+                                            Vec<T, W>& res) {
+  auto& v = L.v;
+  const int nt = ntree_of<NMAX, SHAPE>(A);
+  if constexpr (SCHED == S_LINEAR) {
 #pragma unroll
-  for (int w = 0; w < W; ++w) res[w] = v[0][w];
+    for (int s = 1; s < NMAX; ++s)
+      if (s < nt) vapply<OP, T, W>(v[0], v[0], v[s]);
+  } else {
+    if constexpr (SHAPE == SH_PRE) {
+#pragma unroll
+      for (int s = 0; s < NMAX / 2; ++s)
+        if (s < A.rem) vapply<OP, T, W>(v[s], v[s], L.u[s]);  // inout = odd rank 2s+1
+    }
+    if constexpr (!role_sensitive<OP, T>::v) {
+      fold_tree<OP, T, NMAX, W, 0>(nt, v);
+    } else {
+      if (!A.owner_mode) {
+        fold_tree<OP, T, NMAX, W, 0>(nt, v);
+      } else {
+        const unsigned long long g0 = (unsigned long long)(A.gbase + e);
+        const unsigned j0 = owner_block(A, g0);
+        const unsigned top = (1u << A.pof2_log) - 1;
+        const bool uniform = W == 1 || j0 == top ||
+                             g0 + (W - 1) < (unsigned long long)(j0 + 1) * (unsigned long long)A.blk_len;
+        if (!uniform) return false;
+        fold_tree_own<OP, T, NMAX, W, 0>((int)bitrev(j0, A.pof2_log), nt, v);
+      }
+    }
+  }
+  res = v[0];
+  return true;
+}
+
+template <class OP, class T, int NMAX, int SCHED, int SHAPE, int W>
+__device__ __forceinline__ bool fold_at(const FoldArgs& A, const T* const* src, const T* const* src2,
+                                        long long e, Vec<T, W>& res) {
+  Leaves<T, NMAX, SHAPE, W> L;
+  load_leaves<T, NMAX, SCHED, SHAPE, W>(A, src, src2, e, L);
+  return fold_leaves<OP, T, NMAX, SCHED, SHAPE, W>(A, e, L, res);
+}
+
+// Elements [e, e+k) one at a time into out1 (and out2): the straddling
+// vectors of fold_leaves and ragged tails.  Not unrolled: one copy of the
+// scalar fold.
+template <class OP, class T, int NMAX, int SCHED, int SHAPE>
+__device__ __forceinline__ void fold_elems(const FoldArgs& A, const T* const* src, const T* const* src2, long long e,
+                                        int k, T* out1, T* out2) {
+#pragma unroll 1
+  for (int w = 0; w < k; ++w) {
+    Vec<T, 1> r;
+    fold_at<OP, T, NMAX, SCHED, SHAPE, 1>(A, src, src2, e + w, r);
+    out1[e + w] = r.x[0];
+    if (out2) out2[e + w] = r.x[0];
+  }
 }
 
 // Fold [lo, hi) (element indices into the sources) into out1 (and out2 if
 // non-null), the whole block cooperating.  lo is a multiple of the vector
 // width; `vec` says whether every pointer involved is 16-byte aligned.
-template <class OP, class T, int NMAX, int SCHED>
+template <class OP, class T, int NMAX, int SCHED, int SHAPE>
 __device__ __forceinline__ void fold_range(const FoldArgs& A, const T* const* src, const T* const* src2,
                                            long long lo, long long hi, T* out1, T* out2, bool vec,
                                            long long tid, long long nthr) {
@@ -314,19 +484,17 @@ __device__ __forceinline__ void fold_range(const FoldArgs& A, const T* const* sr
     const long long nv = (hi - lo) / W;
     for (long long i = tid; i < nv; i += nthr) {
       const long long e = lo + i * W;
-      T r[W];
-      fold_at<OP, T, NMAX, SCHED, W>(A, src, src2, e, r);
-      st<T, W>(out1 + e, r);
-      if (out2) st<T, W>(out2 + e, r);
+      Vec<T, W> r;
+      if (fold_at<OP, T, NMAX, SCHED, SHAPE, W>(A, src, src2, e, r)) {
+        stv<T, W>(out1 + e, r);
+        if (out2) stv<T, W>(out2 + e, r);
+      } else {
+        fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, e, W, out1, out2);
+      }
     }
     lo += nv * W;
   }
-  for (long long e = lo + tid; e < hi; e += nthr) {
-    T r[1];
-    fold_at<OP, T, NMAX, SCHED, 1>(A, src, src2, e, r);
-    out1[e] = r[0];
-    if (out2) out2[e] = r[0];
-  }
+  for (long long e = lo + tid; e < hi; e += nthr) fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, e, 1, out1, out2);
 }
 
 // ---------------------------------------------------------------------------
@@ -438,47 +606,78 @@ __device__ __forceinline__ void pull_release(int on) {
 // cross-rank barrier of block `blockIdx.x` on every rank, at epoch `ep`.
 // Producer side: every wave drains its stores, block barrier, one wave issues
 // a SYSTEM-scope release (writes this XCD's L2 back so peers reading our HBM
-// over xGMI see it), then one lane per peer stores `ep` into that peer's
-// signal slot [block][my rank].  Consumer side: lane p polls my slot
-// [block][p] (relaxed, system scope, uncached memory) until >= ep, then a
-// system-scope acquire invalidates this CU's L1 and the stale non-coherent
-// L2 lines before any wave reads peer data (MI355X_MICROARCH.md
+// over xGMI see it), then one lane per peer stores its signal word into that
+// peer's slot [block][my rank].  Consumer side: lane p polls my slot
+// [block][p] (relaxed, system scope, uncached memory) until it reaches `ep`,
+// then a system-scope acquire invalidates this CU's L1 and the stale
+// non-coherent L2 lines before any wave reads peer data (MI355X_MICROARCH.md
 // "inter-workgroup visibility"; cdna_hip_programming.md Guideline 16, at
 // system instead of agent scope because the peers are other GPUs).
-// Epochs are monotone per communicator, so slots never need resetting.
+//
+// Signal word = ep << 25 | abort << 24 | key (24 bits).  Epochs are monotone
+// per communicator, so slots never need resetting.  `abort` (optional, the
+// block's running flag, identical in every thread) is published and ORed with
+// every peer's: once any rank aborts a launch every later barrier of it
+// carries the bit, so all ranks of all blocks learn it by the barrier after.
+// check_key: a peer whose word for THIS epoch carries another key aborts the
+// launch (zero-copy views, mpigx.cpp zc_run: every rank must use the buffer
+// mappings agreed in the same exchange).  A peer already past this epoch has
+// itself compared our word for it, so a mismatch is never missed.
 // Returns false (and sets *err) if a peer did not arrive within the timeout.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep) {
-  __shared__ int s_fail;
+constexpr int kSigShift = 25;
+
+__device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, int* abort = nullptr,
+                                             unsigned key = 0, bool check_key = false) {
+  __shared__ int s_fail, s_abort;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  const int ab_in = abort ? *abort : 0;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bool ok = true;
+    bool ok = true, ab = false;
     if (lane < pv.n) {
+      const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24) | (uint64_t)(key & 0xffffffu);
       uint64_t* peer_slot = pv.sig[lane] + (size_t)blockIdx.x * kMaxRanks + pv.rank;
-      __hip_atomic_store(peer_slot, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(peer_slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       uint64_t* mine = pv.sig[pv.rank] + (size_t)blockIdx.x * kMaxRanks + lane;
       const uint64_t t0 = wall_clock64();
-      while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < ep) {
+      uint64_t v;
+      while (((v = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> kSigShift) < ep) {
         __builtin_amdgcn_s_sleep(1);
         if (wall_clock64() - t0 > pv.timeout_ticks) {
           ok = false;
           break;
         }
       }
+      ab = ok && (((v >> 24) & 1u) || (check_key && (v >> kSigShift) == ep && (v & 0xffffffu) != (key & 0xffffffu)));
     }
     const bool all_ok = __all(ok);
+    const bool any_ab = __any(ab);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (lane == 0) {
       s_fail = all_ok ? 0 : 1;
+      s_abort = (ab_in || any_ab) ? 1 : 0;
       if (!all_ok) __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   __syncthreads();
+  if (abort) *abort = s_abort;
   return s_fail == 0;
+}
+
+// Zero-copy launches (mpigx.cpp zc_run): entry barrier with the view key and
+// this rank's own verdict (pv.zc_bad: no agreed mapping / a failed import).
+__device__ __forceinline__ bool zc_enter(const PeerView& pv, uint64_t ep, int* abort) {
+  *abort = pv.zc_bad;
+  return rank_barrier(pv, ep, abort, pv.zc_key, true);
+}
+// ... and its end: an aborted launch tells the host (which re-resolves).
+__device__ __forceinline__ void zc_leave(const PeerView& pv, int abort) {
+  if (abort && blockIdx.x == 0 && threadIdx.x == 0 && pv.zc_stale)
+    __hip_atomic_store(pv.zc_stale, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace mpigx

@@ -21,14 +21,30 @@ constexpr bool kCplx = is_cplx<T>::v;
 template <class OP>
 hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a) {
   if (a.mode == M_LOCAL) {
-    if (sched == S_LINEAR && nmax <= 8)
-      hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_LINEAR>), grid, dim3(kThreads), 0, s, a);
-    else if (sched == S_LINEAR)
-      hipLaunchKernelGGL((fold_local_kernel<OP, T, 16, S_LINEAR>), grid, dim3(kThreads), 0, s, a);
-    else if (nmax <= 8)
-      hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_TREE>), grid, dim3(kThreads), 0, s, a);
-    else
-      hipLaunchKernelGGL((fold_local_kernel<OP, T, 16, S_TREE>), grid, dim3(kThreads), 0, s, a);
+    // shape and vectors per thread: fold_shape / local_u (common.hpp), the
+    // rule the host sized the grid with
+    constexpr int UF = local_u(MPIGX_REP, OP::code, SH_FULL);
+    const int shape = fold_shape(sched, nmax, a.ntree, a.rem);
+    if (sched == S_LINEAR) {
+      if (nmax > 8)
+        hipLaunchKernelGGL((fold_local_kernel<OP, T, 16, S_LINEAR, SH_POW2, 1>), grid, dim3(kThreads), 0, s, a);
+      else if (shape == SH_FULL)
+        hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_LINEAR, SH_FULL, UF>), grid, dim3(kThreads), 0, s, a);
+      else
+        hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_LINEAR, SH_POW2, 1>), grid, dim3(kThreads), 0, s, a);
+    } else if (nmax <= 8) {
+      if (shape == SH_FULL)
+        hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_TREE, SH_FULL, UF>), grid, dim3(kThreads), 0, s, a);
+      else if (shape == SH_POW2)
+        hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_TREE, SH_POW2, 1>), grid, dim3(kThreads), 0, s, a);
+      else
+        hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_TREE, SH_PRE, 1>), grid, dim3(kThreads), 0, s, a);
+    } else {
+      if (shape == SH_PRE)
+        hipLaunchKernelGGL((fold_local_kernel<OP, T, 16, S_TREE, SH_PRE, 1>), grid, dim3(kThreads), 0, s, a);
+      else
+        hipLaunchKernelGGL((fold_local_kernel<OP, T, 16, S_TREE, SH_POW2, 1>), grid, dim3(kThreads), 0, s, a);
+    }
   } else if (sched == S_LINEAR && nmax <= 8) {
     hipLaunchKernelGGL((fold_kernel<OP, T, 8, S_LINEAR>), grid, dim3(kThreads), 0, s, a);
   } else if (sched == S_LINEAR) {

@@ -69,20 +69,64 @@ __global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
 // ops (float MIN/MAX) made the compiler copy the whole 840-B argument block
 // to scratch in every thread at entry — 16 M threads x 840 B per 256 MiB
 // call held f32 MAX at 0.67 TB/s.  This kernel touches only M_LOCAL fields.
-template <class OP, class T, int NMAX, int SCHED>
+//
+// One pass: thread t of block b folds the U vectors (16 B of every input
+// each) at vector indices (b*U + u)*kThreads + t, all U*ntree loads issued
+// before any arithmetic; the grid covers the whole range (a grid-stride loop
+// only takes over beyond 2^32 threads).  SHAPE: SH_PRE / SH_POW2 / SH_FULL.
+template <class OP, class T, int NMAX, int SCHED, int SHAPE, int U>
 __global__ __launch_bounds__(kThreads) void fold_local_kernel(FoldArgs A) {
+  constexpr int W = VecW<T>::v;
   const T* const* src = reinterpret_cast<const T* const*>(A.src);
   const T* const* src2 = reinterpret_cast<const T* const*>(A.src2);
+  T* out = (T*)A.recv;
   bool vec = ((uintptr_t)A.recv & 15) == 0;
 #pragma unroll
   for (int s = 0; s < NMAX; ++s)
     if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
+  if constexpr (SHAPE == SH_PRE) {
 #pragma unroll
-  for (int s = 0; s < NMAX / 2; ++s)
-    if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
-  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x,
-                  gnt = (long long)gridDim.x * blockDim.x;
-  fold_range<OP, T, NMAX, SCHED>(A, src, src2, 0, A.count, (T*)A.recv, nullptr, vec, gtid, gnt);
+    for (int s = 0; s < NMAX / 2; ++s)
+      if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
+  }
+  const long long tid = threadIdx.x;
+  if (!vec) {
+    const long long gt = (long long)blockIdx.x * kThreads + tid, gn = (long long)gridDim.x * kThreads;
+    fold_range<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, 0, A.count, out, nullptr, false, gt, gn);
+    return;
+  }
+  const long long nv = A.count / W;
+  const long long step = (long long)gridDim.x * (U * kThreads);
+  for (long long v0 = (long long)blockIdx.x * (U * kThreads) + tid; v0 < nv; v0 += step) {
+    if (v0 + (long long)(U - 1) * kThreads < nv) {
+      Leaves<T, NMAX, SHAPE, W> L[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load_leaves<T, NMAX, SCHED, SHAPE, W>(A, src, src2, (v0 + u * kThreads) * W, L[u]);
+      unsigned strad = 0;  // vectors straddling a Rabenseifner block boundary
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long e = (v0 + u * kThreads) * W;
+        Vec<T, W> r;
+        if (fold_leaves<OP, T, NMAX, SCHED, SHAPE, W>(A, e, L[u], r)) stv<T, W>(out + e, r);
+        else strad |= 1u << u;
+      }
+#pragma unroll 1
+      for (int u = 0; u < U; ++u)
+        if ((strad >> u) & 1u) fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, (v0 + u * kThreads) * W, W, out, nullptr);
+    } else {
+#pragma unroll 1
+      for (int u = 0; u < U; ++u)
+        if (v0 + u * kThreads < nv) {
+          const long long e = (v0 + u * kThreads) * W;
+          Vec<T, W> r;
+          if (fold_at<OP, T, NMAX, SCHED, SHAPE, W>(A, src, src2, e, r)) stv<T, W>(out + e, r);
+          else fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, e, W, out, nullptr);
+        }
+    }
+  }
+  // ragged tail (count % W elements): the first thread of block 0
+  if (blockIdx.x == 0 && tid == 0 && nv * W < A.count)
+    fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, nv * W, (int)(A.count - nv * W), out, nullptr);
 }
 
 template <class OP, class T, int NMAX, int SCHED>
@@ -94,20 +138,6 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
   const int b = blockIdx.x;
   const long long tid = threadIdx.x, nt = blockDim.x;
 
-  if (A.mode == M_LOCAL) {
-    bool vec = ((uintptr_t)A.recv & 15) == 0;
-#pragma unroll
-    for (int s = 0; s < NMAX; ++s)
-      if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
-#pragma unroll
-    for (int s = 0; s < NMAX / 2; ++s)
-      if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
-    // grid-stride over the whole range
-    const long long gtid = (long long)b * nt + tid, gnt = (long long)gridDim.x * nt;
-    fold_range<OP, T, NMAX, SCHED>(A, src, src2, 0, A.count, (T*)A.recv, nullptr, vec, gtid, gnt);
-    return;
-  }
-
   T* recv = (T*)A.recv;
   T* mine = (T*)pv.stage[pv.rank];
   const char* send = (const char*)A.send;
@@ -117,8 +147,11 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
 
   if (A.mode == M_AR_ZC) {
     // zero-copy two-shot: no staging; sources are the peers' send buffers
+    // (skipped everywhere if any rank's view of the mappings is stale)
     const int n = pv.n, r = pv.rank;
-    if (!rank_barrier(pv, ep++)) return;  // every rank's send buffer is ready
+    int ab;
+    if (!zc_enter(pv, ep++, &ab)) return;  // every rank's send buffer is ready
+    if (!ab) {
     const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
     const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
     bool vec = recv_vec;
@@ -128,8 +161,10 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
 #pragma unroll
     for (int s = 0; s < NMAX / 2; ++s)
       if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
-    fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
-    if (!rank_barrier(pv, ep++)) return;  // every reduced chunk is in its owner's recvbuf
+    fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
+    }
+    if (!rank_barrier(pv, ep++, &ab)) return;  // every reduced chunk is in its owner's recvbuf
+    if (!ab) {
     char* dsts[NMAX];
     const char* srcs[NMAX];
     long long lens[NMAX];
@@ -148,7 +183,9 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
       }
     }
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
-    rank_barrier(pv, ep++);  // nobody reads my buffers any more
+    }
+    rank_barrier(pv, ep++, &ab);  // nobody reads my buffers any more
+    zc_leave(pv, ab);
     return;
   }
 
@@ -178,7 +215,11 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
       }
     }
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
-    if (!rank_barrier(pv, ep++)) return;
+    // phase 2 writes into the peers' recvbufs through the view's mappings:
+    // the barrier checks every rank uses the same view (zc_enter)
+    int ab = pv.zc_bad;
+    if (!rank_barrier(pv, ep++, &ab, pv.zc_key, true)) return;
+    if (!ab) {
     // phase 2: fold my chunk (slots = local HBM) into my recvbuf, then write
     // the reduced slice into every peer's recvbuf
     const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
@@ -190,7 +231,7 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
 #pragma unroll
     for (int s = 0; s < NMAX / 2; ++s)
       if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
-    fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
+    fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NMAX; ++j) {
@@ -205,7 +246,9 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
       }
     }
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
-    rank_barrier(pv, ep++);  // every slice of my recvbuf has arrived
+    }
+    rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
+    zc_leave(pv, ab);
     return;
   }
 
@@ -214,7 +257,7 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);
     if (!rank_barrier(pv, ep++)) return;
     if (A.mode == M_AR_ONESHOT || pv.rank == A.root)
-      fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
+      fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
     rank_barrier(pv, ep++);
     return;
   }
@@ -235,9 +278,9 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     // staging (for the peers' gather) and straight into my recvbuf.
     const bool want_recv = (A.mode == M_AR_TWOSHOT) || (r == A.root);
     if (want_recv)
-      fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, recv, mine, recv_vec, tid, nt);
+      fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, mine, recv_vec, tid, nt);
     else
-      fold_range<OP, T, NMAX, SCHED>(A, src, src2, lo, hi, mine, nullptr, true, tid, nt);
+      fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, mine, nullptr, true, tid, nt);
   }
   (void)W;
   if (!rank_barrier(pv, ep++)) return;
@@ -276,22 +319,22 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
 // owner, in = other half as computed on owner^half).
 // ---------------------------------------------------------------------------
 template <class OP, class T, int SIZE, int W>
-__device__ __forceinline__ void blk_total(const PeerView& pv, int base, int owner, long long e, T (&out)[W]) {
+__device__ __forceinline__ void blk_total(const PeerView& pv, int base, int owner, long long e, Vec<T, W>& out) {
   if constexpr (SIZE == 1) {
-    ld<T, W>(out, (const T*)pv.stage[base] + e);
+    ldv<T, W>(out, (const T*)pv.stage[base] + e);
   } else {
     constexpr int H = SIZE / 2;
     const bool hi_own = (owner - base) & H;
-    T a[W], c[W];
+    Vec<T, W> a, c;
     blk_total<OP, T, H, W>(pv, base, hi_own ? owner ^ H : owner, e, a);       // low half
     blk_total<OP, T, H, W>(pv, base + H, hi_own ? owner : owner ^ H, e, c);   // high half
-#pragma unroll
-    for (int w = 0; w < W; ++w) out[w] = hi_own ? OP::apply(c[w], a[w]) : OP::apply(a[w], c[w]);
+    if (hi_own) vapply<OP, T, W>(out, c, a);
+    else vapply<OP, T, W>(out, a, c);
   }
 }
 
 template <class OP, class T, int W>
-__device__ __forceinline__ void blk_total_rt(const PeerView& pv, int m, int base, int owner, long long e, T (&out)[W]) {
+__device__ __forceinline__ void blk_total_rt(const PeerView& pv, int m, int base, int owner, long long e, Vec<T, W>& out) {
   switch (m) {
     case 1: blk_total<OP, T, 1, W>(pv, base, owner, e, out); break;
     case 2: blk_total<OP, T, 2, W>(pv, base, owner, e, out); break;
@@ -301,22 +344,20 @@ __device__ __forceinline__ void blk_total_rt(const PeerView& pv, int m, int base
 }
 
 template <class OP, class T, int W>
-__device__ __forceinline__ void scan_at(const ScanArgs& A, long long e, T (&res)[W], bool& have) {
+__device__ __forceinline__ void scan_at(const ScanArgs& A, long long e, Vec<T, W>& res, bool& have) {
   const int q = A.pv.rank;
   have = !A.exclusive;
-  if (!A.exclusive) ld<T, W>(res, (const T*)A.pv.stage[q] + e);
+  if (!A.exclusive) ldv<T, W>(res, (const T*)A.pv.stage[q] + e);
   for (int m = 1; m < A.pv.n; m <<= 1) {
     if (!(q & m)) continue;
     const int d = q ^ m;
-    T t[W];
+    Vec<T, W> t;
     blk_total_rt<OP, T, W>(A.pv, m, d & ~(m - 1), d, e, t);
     if (!have) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) res[w] = t[w];
+      res = t;
       have = true;
     } else {
-#pragma unroll
-      for (int w = 0; w < W; ++w) res[w] = OP::apply(res[w], t[w]);
+      vapply<OP, T, W>(res, res, t);
     }
   }
 }
@@ -348,18 +389,18 @@ __device__ __forceinline__ void scan_body(const ScanArgs& A) {
     if (((uintptr_t)recv & 15) == 0) {
       const long long nv = (hi - lo) / W;
       for (long long i = tid; i < nv; i += nt) {
-        T r[W];
+        Vec<T, W> r;
         bool have;
         scan_at<OP, T, W>(A, lo + i * W, r, have);
-        st<T, W>(recv + lo + i * W, r);
+        stv<T, W>(recv + lo + i * W, r);
       }
       s = lo + nv * W;
     }
     for (long long e = s + tid; e < hi; e += nt) {
-      T r[1];
+      Vec<T, 1> r;
       bool have;
       scan_at<OP, T, 1>(A, e, r, have);
-      recv[e] = r[0];
+      recv[e] = r.x[0];
     }
   }
   rank_barrier(pv, ep++);

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "handles.hpp"
 #include "launch.hpp"
 #include "runtime.hpp"
 
@@ -205,6 +206,7 @@ PeerView make_view(mpigx_comm* c) {
   pv.dcount = c->dcount_dev;
   pv.dbase = c->dcount_total;
   pv.seq = c->launch_seq + 1;
+  pv.zc_stale = c->zc_stale_dev;
   for (int p = 0; p < c->n; ++p) {
     pv.sig[p] = c->peer_sig[p];
     pv.stage[p] = c->peer_stage[p];
@@ -274,10 +276,11 @@ void plan_schedule(mpigx_comm* c, FoldArgs& a, int n, int root, long long count_
   a.owner_mode = 0;
   a.pof2_log = 0;
   a.blk_len = 1;
+  a.blk_inv = 1.0;
   (void)c;
   if (order == MPIGX_ORDER_LINEAR) {
     *sched = S_LINEAR;
-    *nmax = n <= 8 ? 8 : 16;  // NMAX 16 kernels carry an 840-B scratch entry copy
+    *nmax = n <= 8 ? 8 : 16;
     a.ntree = n;
     for (int k = 0; k < n; ++k) a.src[k] = ptrs[k];
     return;
@@ -303,28 +306,26 @@ void plan_schedule(mpigx_comm* c, FoldArgs& a, int n, int root, long long count_
     a.owner_mode = 1;
     a.pof2_log = log2i(pof2);
     a.blk_len = count_total / pof2;
-    *nmax = pof2 <= 8 ? 8 : 16;
+    a.blk_inv = 1.0 / (double)a.blk_len;
+    // NMAX from n, not pof2: n = 9..15 has pof2 = 8 but up to 7 pre-step
+    // partners (the fold reads src2[s] for s < NMAX/2) and n-1 peers to
+    // gather from (the gather phases cover j < NMAX)
+    *nmax = n <= 8 ? 8 : 16;
   }
 }
 
 int host_allgather(mpigx_comm* c, const void* mine, int len, void* out);
 
-// ---- zero-copy registration (large Allreduce) ------------------------------
+// ---- zero-copy registration ---------------------------------------------
 // A user buffer is exported by the IPC handle of the allocation that holds it
 // (hipMemGetAddressRange base) plus an offset; allocations are identified by
 // HIP's unique buffer id, so a freed-and-reused address never aliases a stale
 // import.  Peers' allocations are opened once and kept (LRU-bounded).
 constexpr size_t kZcCache = 64;
+constexpr size_t kZcTuples = 32;
+constexpr size_t kZcViews = 8;
 
-struct ZcBlob {
-  int ok;
-  int pad;
-  unsigned long long id[2];
-  long long off[2];
-  hipIpcMemHandle_t h[2];
-};
-
-bool zc_export(mpigx_comm* c, const void* p, unsigned long long* id, long long* off,
+bool zc_export(mpigx_comm* c, const void* p, char** pbase, unsigned long long* id, long long* off,
                hipIpcMemHandle_t* h) {
   void* base = nullptr;
   size_t size = 0;
@@ -334,6 +335,7 @@ bool zc_export(mpigx_comm* c, const void* p, unsigned long long* id, long long* 
     (void)hipGetLastError();
     return false;
   }
+  *pbase = (char*)base;
   *id = bid;
   *off = (const char*)p - (const char*)base;
   for (auto& r : c->lreg)
@@ -376,71 +378,223 @@ char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemH
       rt::rma_sync(c);
       (void)hipIpcCloseMemHandle(c->imports[oldest].base);
       c->imports.erase(c->imports.begin() + oldest);
+      c->zviews.clear();  // views may point into the closed mapping
     }
   }
   c->imports.push_back({peer, id, (char*)ptr, ++c->tick, 0, h});
   return (char*)ptr;
 }
 
-// Resolves every rank's send/recv pointers (mapped into this process).  Two
-// host exchanges: the export descriptors, then whether every import worked,
-// so all ranks take the same path.  Returns 1 = use zero-copy, 0 = staged,
-// <0 = error code (negated).
-int zc_resolve(mpigx_comm* c, const void* send, void* recv, const char** psend, char** precv) {
+// ---- zero-copy views ---------------------------------------------------------
+// A zero-copy launch reads / writes the peers' USER buffers through IPC
+// mappings.  Which mappings is agreed in an exchange over the shm control
+// plane (every rank's {buffer id, offset, IPC handle} of send and recv); the
+// result is a VIEW: an id (the exchange's sequence number, the same on every
+// rank) and every rank's mapped pointers, cached per rank with the serial
+// number of each rank's (send, recv) registration.
+//
+// Blocking calls do not exchange again when the buffers repeat: every rank
+// launches at once with the most recent view whose entry for itself matches
+// its current buffers, or flagged bad if it has none.  The launch's entry
+// barrier carries the view id and the flag (device.hpp rank_barrier): a
+// mismatch or a flag anywhere aborts the launch on every rank before any
+// peer byte is touched; the host then sees the abort, all ranks exchange and
+// the launch is repeated on the fresh view.  The steady state (the same
+// buffers call after call, as in any training or benchmark loop) costs no
+// host round trip; a change costs one empty launch.  Stream-ordered calls
+// cannot wait for that verdict and always exchange first.
+struct ZcBlob {
+  int ok;
+  unsigned serial;
+  unsigned long long id[2];
+  long long off[2];
+  hipIpcMemHandle_t h[2];
+};
+static_assert(sizeof(ZcBlob) <= 256, "control-plane blob");
+
+// Serial number of my (send, recv) registration; 0 = not exportable.
+unsigned zc_register(mpigx_comm* c, const void* send, void* recv, ZcBlob* mine) {
+  memset(mine, 0, sizeof *mine);
+  char* base[2];
+  if (!zc_export(c, send, &base[0], &mine->id[0], &mine->off[0], &mine->h[0]) ||
+      !zc_export(c, recv, &base[1], &mine->id[1], &mine->off[1], &mine->h[1]))
+    return 0;
+  mine->ok = 1;
+  for (auto& t : c->ztuples)
+    if (t.id[0] == mine->id[0] && t.id[1] == mine->id[1] && t.off[0] == mine->off[0] && t.off[1] == mine->off[1] &&
+        t.base[0] == base[0] && t.base[1] == base[1] && !memcmp(t.h, mine->h, sizeof t.h)) {
+      t.tick = ++c->tick;
+      mine->serial = t.serial;
+      return t.serial;
+    }
+  if (c->ztuples.size() >= kZcTuples) {
+    size_t old = 0;
+    for (size_t i = 1; i < c->ztuples.size(); ++i)
+      if (c->ztuples[i].tick < c->ztuples[old].tick) old = i;
+    c->ztuples.erase(c->ztuples.begin() + old);
+  }
+  mpigx_comm::ZcTuple t;
+  memset(&t, 0, sizeof t);
+  for (int k = 0; k < 2; ++k) {
+    t.base[k] = base[k];
+    t.id[k] = mine->id[k];
+    t.off[k] = mine->off[k];
+    t.h[k] = mine->h[k];
+  }
+  t.serial = ++c->zserial;
+  t.tick = ++c->tick;
+  c->ztuples.push_back(t);
+  mine->serial = t.serial;
+  return t.serial;
+}
+
+struct ZcLaunch {
+  const char* ps[kMaxRanks];
+  char* pr[kMaxRanks];
+  unsigned key;
+  int bad;
+};
+
+// The optimistic launch's pointers: the most recent view in which my entry
+// is my current registration; bad = 1 (the launch aborts) if there is none.
+void zc_optimistic(mpigx_comm* c, const void* send, void* recv, ZcLaunch* z) {
+  memset(z, 0, sizeof *z);
+  ZcBlob mine;
+  const unsigned ser = zc_register(c, send, recv, &mine);
+  const mpigx_comm::ZcView* best = nullptr;
+  if (ser)
+    for (auto& v : c->zviews)
+      if (v.serial[c->rank] == ser && (!best || v.tick > best->tick)) best = &v;
+  if (!best) {
+    z->bad = 1;
+    return;
+  }
+  for (int q = 0; q < c->n; ++q) {
+    z->ps[q] = best->ps[q];
+    z->pr[q] = best->pr[q];
+  }
+  z->ps[c->rank] = (const char*)send;
+  z->pr[c->rank] = (char*)recv;
+  z->key = best->id;
+}
+
+// Exchange: every rank's registration, imports, a new view.  Returns 1 =
+// launch with *z (z->bad = 1 if an import failed here: the launch aborts on
+// every rank and reports MPI_ERR_INTERN), 0 = some rank's buffer is not
+// exportable (every rank takes the staged path), < 0 = -error.
+int zc_exchange(mpigx_comm* c, const void* send, void* recv, ZcLaunch* z) {
+  memset(z, 0, sizeof *z);
   const int n = c->n;
   ZcBlob mine;
-  memset(&mine, 0, sizeof mine);
-  mine.ok = zc_export(c, send, &mine.id[0], &mine.off[0], &mine.h[0]) &&
-            zc_export(c, recv, &mine.id[1], &mine.off[1], &mine.h[1]);
-  static_assert(sizeof(ZcBlob) <= 256, "control-plane blob");
+  zc_register(c, send, recv, &mine);
   ZcBlob all[kMaxRanks];
-  int rc = host_allgather(c, &mine, sizeof mine, all);
+  const int rc = host_allgather(c, &mine, sizeof mine, all);
   if (rc) return -rc;
+  c->zstat_exchanges++;
+  const unsigned id = (++c->zview_seq) & 0xffffffu;
   for (int q = 0; q < n; ++q)
     if (!all[q].ok) return 0;
-  int ok = 1;
-  for (int q = 0; q < n && ok; ++q) {
+  mpigx_comm::ZcView v;
+  memset(&v, 0, sizeof v);
+  v.id = id;
+  bool ok = true;
+  for (int q = 0; q < n; ++q) {
+    v.serial[q] = all[q].serial;
     if (q == c->rank) {
-      psend[q] = (const char*)send;
-      precv[q] = (char*)recv;
+      v.ps[q] = (const char*)send;
+      v.pr[q] = (char*)recv;
       continue;
     }
     char* sb = zc_import(c, q, all[q].id[0], all[q].h[0]);
     char* rb = all[q].id[1] == all[q].id[0] ? sb : zc_import(c, q, all[q].id[1], all[q].h[1]);
     if (!sb || !rb) {
-      ok = 0;
+      ok = false;
       break;
     }
-    psend[q] = sb + all[q].off[0];
-    precv[q] = rb + all[q].off[1];
+    v.ps[q] = sb + all[q].off[0];
+    v.pr[q] = rb + all[q].off[1];
   }
-  int oks[kMaxRanks];
-  rc = host_allgather(c, &ok, sizeof ok, oks);
-  if (rc) return -rc;
-  for (int q = 0; q < n; ++q)
-    if (!oks[q]) return 0;
+  if (!ok) {
+    z->bad = 1;
+    z->key = id;
+    return 1;
+  }
+  v.tick = ++c->tick;
+  if (c->zviews.size() >= kZcViews) {
+    size_t old = 0;
+    for (size_t i = 1; i < c->zviews.size(); ++i)
+      if (c->zviews[i].tick < c->zviews[old].tick) old = i;
+    c->zviews.erase(c->zviews.begin() + old);
+  }
+  c->zviews.push_back(v);
+  for (int q = 0; q < n; ++q) {
+    z->ps[q] = v.ps[q];
+    z->pr[q] = v.pr[q];
+  }
+  z->key = id;
   return 1;
+}
+
+bool zc_take_stale(mpigx_comm* c) {
+  if (!__atomic_load_n(c->zc_stale, __ATOMIC_ACQUIRE)) return false;
+  __atomic_store_n(c->zc_stale, 0u, __ATOMIC_RELEASE);
+  return true;
+}
+
+// Runs one zero-copy collective: `launch(z)` enqueues its kernel(s) with
+// view z on every rank (identical grids everywhere).  Returns an error, or
+// MPIGX_SUCCESS with *staged = true when the caller must run the staged
+// algorithm instead (some rank's buffer cannot be exported).
+template <class F>
+int zc_run(mpigx_comm* c, const void* send, void* recv, bool* staged, F&& launch) {
+  *staged = false;
+  ZcLaunch z;
+  if (c->blocking && c->zc_optimistic) {
+    zc_optimistic(c, send, recv, &z);
+    int rc = launch(z);
+    if (!rc) rc = finish(c);
+    if (rc) return rc;
+    if (!zc_take_stale(c)) {
+      c->zstat_hits++;
+      return MPIGX_SUCCESS;
+    }
+  }
+  const int r = zc_exchange(c, send, recv, &z);
+  if (r < 0) return -r;
+  if (r == 0) {
+    *staged = true;
+    return MPIGX_SUCCESS;
+  }
+  int rc = launch(z);
+  if (!rc) rc = finish(c);
+  if (!rc && zc_take_stale(c)) rc = MPIGX_ERR_INTERN;  // an import failed on some rank
+  return rc;
+}
+
+void zc_apply(PeerView& pv, const ZcLaunch& z) {
+  pv.zc_key = z.key;
+  pv.zc_bad = z.bad;
 }
 
 // Zero-copy two-shot Allreduce over the whole message (no rounds: nothing is
 // staged).  Same chunk/slice partition and fold schedule as M_AR_TWOSHOT.
-int allreduce_zc(mpigx_comm* c, const char* const* psend, char* const* precv, long long count,
-                 const TypeInfo* t, int oc) {
+int allreduce_zc(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeInfo* t, int oc) {
   const int n = c->n, es = t->size;
   const int vec = es >= 16 ? 1 : 16 / es;
   FoldArgs a;
   memset(&a, 0, sizeof a);
   a.pv = make_view(c);
+  zc_apply(a.pv, z);
   a.mode = M_AR_ZC;
   a.esize = es;
   a.count = count;
   a.gbase = 0;
-  a.send = psend[c->rank];
-  a.recv = precv[c->rank];
-  for (int p = 0; p < n; ++p) a.zc_recv[p] = precv[p];
+  a.send = z.ps[c->rank];
+  a.recv = z.pr[c->rank];
+  for (int p = 0; p < n; ++p) a.zc_recv[p] = z.pr[p];
   int nmax, sched;
   const void* ptrs[kMaxRanks];
-  for (int p = 0; p < n; ++p) ptrs[p] = psend[p];
+  for (int p = 0; p < n; ++p) ptrs[p] = z.ps[p];
   plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
   a.chunk = rup(cdiv(count, n), vec);
   const int grid = grid_for(c, a.chunk * es);
@@ -448,7 +602,7 @@ int allreduce_zc(mpigx_comm* c, const char* const* psend, char* const* precv, lo
   HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
   note_launch(c, a.pv, grid);
   c->epoch += 3;
-  return finish(c);
+  return MPIGX_SUCCESS;
 }
 
 // Push two-shot Allreduce (MPIGX_ALGO=push; needs the zero-copy mapping of
@@ -456,8 +610,7 @@ int allreduce_zc(mpigx_comm* c, const char* const* psend, char* const* precv, lo
 // arena; per round: my chunk p -> rank p's slot [me] (remote stores), barrier,
 // fold my chunk from my slots + my sendbuf (same schedule as every other
 // path, so the same bits), result -> every rank's recvbuf, barrier.
-int allreduce_push(mpigx_comm* c, const void* send, char* const* precv, long long count, const TypeInfo* t,
-                   int oc) {
+int allreduce_push(mpigx_comm* c, const ZcLaunch& z, const void* send, long long count, const TypeInfo* t, int oc) {
   const int n = c->n, r = c->rank, es = t->size;
   const int vec = es >= 16 ? 1 : 16 / es;
   long long round = (long long)(c->stage_bytes / es);
@@ -467,13 +620,14 @@ int allreduce_push(mpigx_comm* c, const void* send, char* const* precv, long lon
     FoldArgs a;
     memset(&a, 0, sizeof a);
     a.pv = make_view(c);
+    zc_apply(a.pv, z);
     a.mode = M_AR_PUSH;
     a.esize = es;
     a.count = cnt;
     a.gbase = off;
     a.send = (const char*)send + off * es;
-    a.recv = precv[r] + off * es;
-    for (int p = 0; p < n; ++p) a.zc_recv[p] = precv[p] + off * es;
+    a.recv = z.pr[r] + off * es;
+    for (int p = 0; p < n; ++p) a.zc_recv[p] = z.pr[p] ? z.pr[p] + off * es : nullptr;
     a.chunk = rup(cdiv(cnt, n), vec);
     a.slot_bytes = a.chunk * es;
     // leaf q of my chunk: slot q of my arena holds rank q's copy of it
@@ -491,7 +645,7 @@ int allreduce_push(mpigx_comm* c, const void* send, char* const* precv, long lon
     note_launch(c, a.pv, grid);
     c->epoch += 2;
   }
-  return finish(c);
+  return MPIGX_SUCCESS;
 }
 
 // Shared driver for Allreduce / Reduce.
@@ -507,12 +661,12 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   // count and the thresholds are identical on every rank, so is this test
   if (all && n > 1 && c->zc_min > 0 && count * es >= c->zc_min &&
       !(algo_env && !strcmp(algo_env, "oneshot"))) {
-    const char* ps[kMaxRanks];
-    char* pr[kMaxRanks];
-    const int z = zc_resolve(c, send, recv, ps, pr);
-    if (z < 0) return -z;
-    if (z == 1 && algo_env && !strcmp(algo_env, "push")) return allreduce_push(c, send, pr, count, t, oc);
-    if (z == 1) return allreduce_zc(c, ps, pr, count, t, oc);
+    const bool push = algo_env && !strcmp(algo_env, "push");
+    bool staged;
+    const int rc = zc_run(c, send, recv, &staged, [&](const ZcLaunch& z) {
+      return push ? allreduce_push(c, z, send, count, t, oc) : allreduce_zc(c, z, count, t, oc);
+    });
+    if (rc || !staged) return rc;
     if (c->zc_require) return MPIGX_ERR_INTERN;  // tests: the path must not fall back
   }
   for (long long off = 0; off < count; off += round) {
@@ -693,7 +847,8 @@ int dtype_size(int datatype) {
   return t ? t->size : -1;
 }
 bool export_buf(mpigx_comm* c, const void* p, unsigned long long* id, long long* off, hipIpcMemHandle_t* h) {
-  return zc_export(c, p, id, off, h);
+  char* base;
+  return zc_export(c, p, &base, id, off, h);
 }
 char* import_buf(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h) {
   return zc_import(c, peer, id, h);
@@ -813,19 +968,40 @@ int mpigx_get_unique_id(mpigx_unique_id_t* id) {
   return MPIGX_SUCCESS;
 }
 
-int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t* id, int rank, int device) {
-  if (!out || !id) return MPIGX_ERR_ARG;
-  if (nranks < 1 || nranks > kMaxRanks) return MPIGX_ERR_ARG;
-  if (rank < 0 || rank >= nranks) return MPIGX_ERR_ARG;
-  IdPayload p;
-  memcpy(&p, id->internal, sizeof p);
-  if (p.magic != kMagic) return MPIGX_ERR_ARG;
-  HIPCK(hipSetDevice(device));
+}  // extern "C"
 
-  mpigx_comm* c = new mpigx_comm();
-  c->rank = rank;
-  c->n = nranks;
-  c->device = device;
+namespace {
+
+// Frees whatever a (possibly half-built) communicator holds: the device
+// allocations, the pinned page, peer mappings and the shm block.  Used by
+// mpigx_comm_free after its closing barrier and by every failed init.
+void comm_release(mpigx_comm* c) {
+  (void)hipSetDevice(c->device);
+  if (c->stream || c->launch_seq) (void)hipStreamSynchronize(c->stream);
+  rt::rma_destroy(c);
+  rt::p2p_destroy(c);
+  for (int q = 0; q < c->n; ++q) {
+    if (c->peer_opened[q]) (void)hipIpcCloseMemHandle(c->peer_stage[q]);
+    if (c->peer_sig_opened[q]) (void)hipIpcCloseMemHandle(c->peer_sig[q]);
+  }
+  for (auto& im : c->imports) (void)hipIpcCloseMemHandle(im.base);
+  if (c->shm) munmap(c->shm, sizeof(ShmBlock));
+  for (auto& b : c->tmp_free) (void)hipFree(b.second);
+  for (auto& b : c->tmp_used) (void)hipFree(b.second);
+  if (c->stage) (void)hipFree(c->stage);
+  if (c->sig) (void)hipFree(c->sig);
+  if (c->dcount_dev) (void)hipFree(c->dcount_dev);
+  if (c->err) (void)hipHostFree(c->err);
+  (void)hipGetLastError();
+  delete c;
+}
+
+// Builds communicator c (allocations, then the shm rendezvous and the IPC
+// mappings of every peer's arena and signal array).  On failure returns the
+// error with c holding whatever was acquired so far; *shm_created tells the
+// caller it must unlink the shm name (rank 0 before every rank mapped it).
+int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
+  const int rank = c->rank, nranks = c->n, device = c->device;
   c->max_blocks = (int)env_ll("MPIGX_MAX_BLOCKS", 256);
   if (c->max_blocks < 1) c->max_blocks = 1;
   if (c->max_blocks > kMaxBlocks) c->max_blocks = kMaxBlocks;
@@ -849,89 +1025,129 @@ int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t*
   HIPCK(hipHostGetDevicePointer((void**)&c->err_dev, c->err, 0));
   c->done = (volatile unsigned long long*)(c->err + 8);  // same pinned page, own 32-B slot
   HIPCK(hipHostGetDevicePointer((void**)&c->done_dev, (void*)c->done, 0));
+  c->zc_stale = c->err + 4;  // byte 16: set by an aborted zero-copy launch
+  HIPCK(hipHostGetDevicePointer((void**)&c->zc_stale_dev, (void*)c->zc_stale, 0));
+  c->zc_optimistic = env_ll("MPIGX_ZC_OPTIMISTIC", 1) != 0;
   c->sync_mode = (int)env_ll("MPIGX_SYNC_SPIN", 1);
   HIPCK(hipMalloc((void**)&c->dcount_dev, 64));
   HIPCK(hipMemset(c->dcount_dev, 0, 64));
   HIPCK(hipDeviceSynchronize());
   c->peer_stage[rank] = c->stage;
   c->peer_sig[rank] = c->sig;
+  if (nranks == 1) return MPIGX_SUCCESS;
 
-  if (nranks > 1) {
-    // rendezvous
-    const double t0 = now_s();
-    const double limit = env_ll("MPIGX_INIT_TIMEOUT_MS", 120000) / 1000.0;
-    int fd = -1;
-    if (rank == 0) {
-      fd = shm_open(p.name, O_CREAT | O_EXCL | O_RDWR, 0600);
-      if (fd < 0 || ftruncate(fd, sizeof(ShmBlock)) != 0) {
-        fprintf(stderr, "[mpigx] shm_open(%s): %s\n", p.name, strerror(errno));
-        return MPIGX_ERR_INTERN;
-      }
-    } else {
-      while ((fd = shm_open(p.name, O_RDWR, 0600)) < 0) {
-        if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
-        usleep(1000);
-      }
-      struct stat st;
-      while (fstat(fd, &st) == 0 && (size_t)st.st_size < sizeof(ShmBlock)) {
-        if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
-        usleep(1000);
-      }
+  // rendezvous
+  const double t0 = now_s();
+  const double limit = env_ll("MPIGX_INIT_TIMEOUT_MS", 120000) / 1000.0;
+  int fd = -1;
+  if (rank == 0) {
+    fd = shm_open(p.name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd >= 0) *shm_created = true;
+    if (fd < 0 || ftruncate(fd, sizeof(ShmBlock)) != 0) {
+      fprintf(stderr, "[mpigx] shm_open(%s): %s\n", p.name, strerror(errno));
+      if (fd >= 0) close(fd);
+      return MPIGX_ERR_INTERN;
     }
-    void* m = mmap(nullptr, sizeof(ShmBlock), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    close(fd);
-    if (m == MAP_FAILED) return MPIGX_ERR_INTERN;
-    c->shm = (ShmBlock*)m;
-    if (rank == 0) {
-      c->shm->nranks = nranks;
-      c->shm->magic.store(kMagic, std::memory_order_release);
-    } else {
-      while (c->shm->magic.load(std::memory_order_acquire) != kMagic) {
-        if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
-        usleep(1000);
-      }
-      if (c->shm->nranks != nranks) return MPIGX_ERR_ARG;
-    }
-    ShmRank& me = c->shm->ranks[rank];
-    me.pid = getpid();
-    me.device = device;
-    hipDeviceProp_t prop;
-    HIPCK(hipGetDeviceProperties(&prop, device));
-    me.pci_bus = prop.pciBusID;
-    me.pci_dev = prop.pciDeviceID;
-    me.stage_bytes = c->stage_bytes;
-    me.stage_ptr = (unsigned long long)(uintptr_t)c->stage;
-    me.sig_ptr = (unsigned long long)(uintptr_t)c->sig;
-    HIPCK(hipIpcGetMemHandle(&me.stage_h, c->stage));
-    HIPCK(hipIpcGetMemHandle(&me.sig_h, c->sig));
-    c->shm->arrived.fetch_add(1, std::memory_order_acq_rel);
-    while (c->shm->arrived.load(std::memory_order_acquire) < nranks) {
+  } else {
+    while ((fd = shm_open(p.name, O_RDWR, 0600)) < 0) {
       if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
-      usleep(200);
+      usleep(1000);
     }
-    for (int q = 0; q < nranks; ++q) {
-      if (q == rank) continue;
-      const ShmRank& pr = c->shm->ranks[q];
-      if (pr.stage_bytes != c->stage_bytes) return MPIGX_ERR_ARG;  // MPIGX_STAGING_BYTES must agree
-      if (pr.pid == me.pid) {
-        c->peer_stage[q] = (char*)(uintptr_t)pr.stage_ptr;
-        c->peer_sig[q] = (uint64_t*)(uintptr_t)pr.sig_ptr;
-      } else {
-        void* ps = nullptr;
-        void* pg = nullptr;
-        HIPCK(hipIpcOpenMemHandle(&ps, pr.stage_h, hipIpcMemLazyEnablePeerAccess));
-        HIPCK(hipIpcOpenMemHandle(&pg, pr.sig_h, hipIpcMemLazyEnablePeerAccess));
-        c->peer_stage[q] = (char*)ps;
-        c->peer_sig[q] = (uint64_t*)pg;
-        c->peer_opened[q] = true;
+    struct stat st;
+    while (fstat(fd, &st) == 0 && (size_t)st.st_size < sizeof(ShmBlock)) {
+      if (now_s() - t0 > limit) {
+        close(fd);
+        return MPIGX_ERR_OTHER;
       }
+      usleep(1000);
     }
-    c->shm->connected.fetch_add(1, std::memory_order_acq_rel);
-    while (c->shm->connected.load(std::memory_order_acquire) < nranks) {
+  }
+  void* m = mmap(nullptr, sizeof(ShmBlock), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) return MPIGX_ERR_INTERN;
+  c->shm = (ShmBlock*)m;
+  if (rank == 0) {
+    c->shm->nranks = nranks;
+    c->shm->magic.store(kMagic, std::memory_order_release);
+  } else {
+    while (c->shm->magic.load(std::memory_order_acquire) != kMagic) {
       if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
-      usleep(200);
+      usleep(1000);
     }
-    if (rank == 0) shm_unlink(p.name);  // every rank has it mapped now
+    if (c->shm->nranks != nranks) return MPIGX_ERR_ARG;
+  }
+  ShmRank& me = c->shm->ranks[rank];
+  me.pid = getpid();
+  me.device = device;
+  hipDeviceProp_t prop;
+  HIPCK(hipGetDeviceProperties(&prop, device));
+  me.pci_bus = prop.pciBusID;
+  me.pci_dev = prop.pciDeviceID;
+  me.stage_bytes = c->stage_bytes;
+  me.stage_ptr = (unsigned long long)(uintptr_t)c->stage;
+  me.sig_ptr = (unsigned long long)(uintptr_t)c->sig;
+  HIPCK(hipIpcGetMemHandle(&me.stage_h, c->stage));
+  HIPCK(hipIpcGetMemHandle(&me.sig_h, c->sig));
+  c->shm->arrived.fetch_add(1, std::memory_order_acq_rel);
+  while (c->shm->arrived.load(std::memory_order_acquire) < nranks) {
+    if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
+    usleep(200);
+  }
+  for (int q = 0; q < nranks; ++q) {
+    if (q == rank) continue;
+    const ShmRank& pr = c->shm->ranks[q];
+    if (pr.stage_bytes != c->stage_bytes) return MPIGX_ERR_ARG;  // MPIGX_STAGING_BYTES must agree
+    c->same_device[q] = pr.pci_bus == me.pci_bus && pr.pci_dev == me.pci_dev;
+    if (pr.pid == me.pid) {
+      c->peer_stage[q] = (char*)(uintptr_t)pr.stage_ptr;
+      c->peer_sig[q] = (uint64_t*)(uintptr_t)pr.sig_ptr;
+    } else {
+      void* ps = nullptr;
+      void* pg = nullptr;
+      HIPCK(hipIpcOpenMemHandle(&ps, pr.stage_h, hipIpcMemLazyEnablePeerAccess));
+      c->peer_stage[q] = (char*)ps;
+      c->peer_opened[q] = true;
+      HIPCK(hipIpcOpenMemHandle(&pg, pr.sig_h, hipIpcMemLazyEnablePeerAccess));
+      c->peer_sig[q] = (uint64_t*)pg;
+      c->peer_sig_opened[q] = true;
+    }
+  }
+  c->shm->connected.fetch_add(1, std::memory_order_acq_rel);
+  while (c->shm->connected.load(std::memory_order_acquire) < nranks) {
+    if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
+    usleep(200);
+  }
+  if (rank == 0) {
+    shm_unlink(p.name);  // every rank has it mapped now
+    *shm_created = false;
+  }
+  return MPIGX_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t* id, int rank, int device) {
+  if (!out || !id) return MPIGX_ERR_ARG;
+  if (nranks < 1 || nranks > kMaxRanks) return MPIGX_ERR_ARG;
+  if (rank < 0 || rank >= nranks) return MPIGX_ERR_ARG;
+  IdPayload p;
+  memcpy(&p, id->internal, sizeof p);
+  if (p.magic != kMagic) return MPIGX_ERR_ARG;
+  HIPCK(hipSetDevice(device));
+  mpigx_comm* c = new mpigx_comm();
+  c->rank = rank;
+  c->n = nranks;
+  c->device = device;
+  bool created = false;
+  const int rc = comm_init(c, p, &created);
+  if (rc) {
+    // nothing outlives a failed init: no allocation, mapping or shm name
+    if (created) shm_unlink(p.name);
+    c->broken = true;
+    comm_release(c);
+    return rc;
   }
   *out = c;
   return MPIGX_SUCCESS;
@@ -949,22 +1165,7 @@ int mpigx_comm_free(mpigx_comm_t c) {
     c->blocking = b;
   }
   (void)hipStreamSynchronize(c->stream);
-  rt::rma_destroy(c);
-  rt::p2p_destroy(c);
-  for (int q = 0; q < c->n; ++q) {
-    if (!c->peer_opened[q]) continue;
-    (void)hipIpcCloseMemHandle(c->peer_stage[q]);
-    (void)hipIpcCloseMemHandle(c->peer_sig[q]);
-  }
-  for (auto& im : c->imports) (void)hipIpcCloseMemHandle(im.base);
-  if (c->shm) munmap(c->shm, sizeof(ShmBlock));
-  for (auto& b : c->tmp_free) (void)hipFree(b.second);
-  for (auto& b : c->tmp_used) (void)hipFree(b.second);
-  (void)hipFree(c->stage);
-  (void)hipFree(c->sig);
-  (void)hipFree(c->dcount_dev);
-  (void)hipHostFree(c->err);
-  delete c;
+  comm_release(c);
   return rc;
 }
 
@@ -1051,6 +1252,12 @@ int mpigx_comm_synchronize(mpigx_comm_t c) {
   rc = finish(c);
   c->blocking = b;
   return rc;
+}
+int mpigx_comm_zc_stats(mpigx_comm_t c, unsigned long long* optimistic_hits, unsigned long long* exchanges) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (optimistic_hits) *optimistic_hits = c->zstat_hits;
+  if (exchanges) *exchanges = c->zstat_exchanges;
+  return MPIGX_SUCCESS;
 }
 int mpigx_comm_set_reduce_order(mpigx_comm_t c, int order) {
   if (!c) return MPIGX_ERR_COMM;
@@ -1175,18 +1382,16 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
   // copy-in, no rounds).  IN_PLACE is given by every rank or none (MPI), and
   // (bytes, n, thresholds) agree, so every rank takes the same branch.
   if (alltoall && !inplace && c->zc_min > 0 && bytes * n >= c->zc_min) {
-    const char* ps[kMaxRanks];
-    char* pr[kMaxRanks];
-    const int z = zc_resolve(c, s, recv, ps, pr);
-    if (z < 0) return -z;
-    if (z == 1) {
+    bool staged;
+    const int rc = zc_run(c, s, recv, &staged, [&](const ZcLaunch& z) {
       CopyArgs a;
       memset(&a, 0, sizeof a);
       a.pv = make_view(c);
+      zc_apply(a.pv, z);
       a.mode = C_ALLTOALL_ZC;
       a.bytes = bytes;
       a.total = bytes;
-      for (int p = 0; p < n; ++p) a.zsrc[p] = ps[p];
+      for (int p = 0; p < n; ++p) a.zsrc[p] = z.ps[p];
       const int g = grid_for(c, bytes * n);
       a.slice = rup(cdiv(bytes, g), 16);
       a.send = s;
@@ -1194,8 +1399,9 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
       HIPCK(launch_copy(dim3(g), c->stream, a));
       note_launch(c, a.pv, g);
       c->epoch += 2;
-      return finish(c);
-    }
+      return MPIGX_SUCCESS;
+    });
+    if (rc || !staged) return rc;
     if (c->zc_require) return MPIGX_ERR_INTERN;
   }
   // rounds: allgather stages `bytes` per rank; alltoall stages n*round
@@ -1590,15 +1796,12 @@ struct UserOp {
   mpigx_device_function* dev_fn;
   int commute;
 };
-static std::vector<UserOp*> g_userops;
-constexpr int kUserOpTag = (int)0x98000000u;  // MPICH HANDLE_KIND_DIRECT | MPID_OP
-constexpr int kUserOpMask = 0x03ffffff;
+// libmpigx's own op handle space (handles.hpp): an op MPI.jl created in libmpi
+// (MPICH user op 0x98000000 | k) never resolves to one of ours — it is not a
+// predefined op either, so it is rejected with MPI_ERR_OP
+static Registry<UserOp, HS_OP> g_userops;
 
-static UserOp* user_op(int h) {
-  if ((h & (int)0xfc000000u) != kUserOpTag) return nullptr;
-  const int i = h & kUserOpMask;
-  return i < (int)g_userops.size() ? g_userops[i] : nullptr;
-}
+static UserOp* user_op(int h) { return g_userops.get(h); }
 
 // kind: 0 allreduce, 1 reduce, 2 scan, 3 exscan
 static int user_reduce(mpigx_comm* c, UserOp* u, const void* send, void* recv, int count, int datatype, int root, int kind) {
@@ -1784,14 +1987,17 @@ int mpigx_reduce_local_multi(const void* const* in, int nin, void* out, long lon
   a.recv = out;
   int nmax, sched;
   plan_schedule(nullptr, a, nin, 0, count, t->size, in, &nmax, &sched, order);
-  // grid: one 16-byte vector per thread, the whole range in ONE pass (no
-  // grid-stride loop).  Measured on MI355X (tools/local_tune.hip, 8 x 256 MiB
-  // f32): one pass 6.0-6.1 TB/s vs 4.8-5.6 TB/s for grid-stride loops over
-  // 1792-16384 blocks — short-lived waves dispatched in address order keep
-  // the 9 streams sequential in DRAM.
+  // grid: U 16-byte vectors per thread (fold_shape / local_u, the rule the
+  // launcher instantiates with), the whole range in ONE pass.  Measured on MI355X
+  // (tools/local_tune.hip, 8 x 256 MiB f32): one pass 6.0-6.1 TB/s vs
+  // 4.8-5.6 TB/s for grid-stride loops over 1792-16384 blocks — short-lived
+  // waves dispatched in address order keep the 9 streams sequential in DRAM.
+  // The kernel strides over the grid only past HIP's 2^32-thread limit.
   const int vec = t->size >= 16 ? 1 : 16 / t->size;
-  long long g = cdiv(cdiv(count, vec), kThreads);
-  const long long cap = env_ll("MPIGX_LOCAL_MAX_BLOCKS", 1ll << 30);
+  const int u = local_u(t->rep, oc, fold_shape(sched, nmax, a.ntree, a.rem));
+  long long g = cdiv(cdiv(count, vec), (long long)kThreads * u);
+  long long cap = env_ll("MPIGX_LOCAL_MAX_BLOCKS", 0xffffffffll / kThreads);
+  if (cap > 0xffffffffll / kThreads) cap = 0xffffffffll / kThreads;
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   FoldLauncher L = fold_launcher(t->rep);
@@ -1812,23 +2018,27 @@ int mpigx_reduce_local(const void* inbuf, void* inoutbuf, int count, int datatyp
   return MPIGX_SUCCESS;
 }
 
+static int op_register(UserOp* u, int* op) {
+  const int h = g_userops.add(u);
+  if (!h) {
+    delete u;
+    return MPIGX_ERR_NO_MEM;
+  }
+  *op = h;
+  return MPIGX_SUCCESS;
+}
 int mpigx_op_create(mpigx_user_function* fn, int commute, int* op) {
   if (!fn || !op) return MPIGX_ERR_ARG;
-  g_userops.push_back(new UserOp{fn, nullptr, commute});
-  *op = kUserOpTag | (int)(g_userops.size() - 1);
-  return MPIGX_SUCCESS;
+  return op_register(new UserOp{fn, nullptr, commute}, op);
 }
 int mpigx_op_create_device(mpigx_device_function* fn, int commute, int* op) {
   if (!fn || !op) return MPIGX_ERR_ARG;
-  g_userops.push_back(new UserOp{nullptr, fn, commute});
-  *op = kUserOpTag | (int)(g_userops.size() - 1);
-  return MPIGX_SUCCESS;
+  return op_register(new UserOp{nullptr, fn, commute}, op);
 }
 int mpigx_op_free(int* op) {
   if (!op) return MPIGX_ERR_ARG;
-  UserOp* u = user_op(*op);
-  if (!u) return MPIGX_ERR_OP;  // predefined ops cannot be freed
-  g_userops[*op & kUserOpMask] = nullptr;
+  UserOp* u = g_userops.remove(*op);
+  if (!u) return MPIGX_ERR_OP;  // predefined, foreign or already freed
   delete u;
   *op = 0x18000000;  // MPI_OP_NULL
   return MPIGX_SUCCESS;

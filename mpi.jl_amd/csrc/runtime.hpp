@@ -148,6 +148,30 @@ struct mpigx_comm {
     int pins;  // RMA windows holding this mapping (never evicted while > 0)
     hipIpcMemHandle_t h;
   };
+  // zero-copy views (mpigx.cpp zc_run): my recent (send, recv) registrations
+  // and the agreed peer mappings of recent exchanges
+  struct ZcTuple {
+    char* base[2];
+    unsigned long long id[2];
+    long long off[2];
+    hipIpcMemHandle_t h[2];
+    unsigned serial;
+    unsigned long long tick;
+  };
+  struct ZcView {
+    unsigned id;                            // exchange sequence number (the launch key)
+    unsigned serial[mpigx::kMaxRanks];      // every rank's registration serial
+    const char* ps[mpigx::kMaxRanks];       // every rank's sendbuf, mapped here
+    char* pr[mpigx::kMaxRanks];             // every rank's recvbuf, mapped here
+    unsigned long long tick;
+  };
+  std::vector<ZcTuple> ztuples;
+  std::vector<ZcView> zviews;
+  unsigned zserial = 0, zview_seq = 0;
+  unsigned* zc_stale = nullptr;      // host-pinned word, set by an aborted zero-copy launch
+  unsigned* zc_stale_dev = nullptr;
+  bool zc_optimistic = true;         // MPIGX_ZC_OPTIMISTIC (blocking calls only)
+  unsigned long long zstat_hits = 0, zstat_exchanges = 0;
   std::vector<LocalReg> lreg;
   std::vector<std::pair<long long, char*>> tmp_free, tmp_used;  // derived-type pack temporaries
   std::vector<Import> imports;
@@ -157,7 +181,9 @@ struct mpigx_comm {
   // peers (index = rank; self included)
   char* peer_stage[mpigx::kMaxRanks] = {};
   uint64_t* peer_sig[mpigx::kMaxRanks] = {};
-  bool peer_opened[mpigx::kMaxRanks] = {};
+  bool peer_opened[mpigx::kMaxRanks] = {};      // peer_stage[q] is an IPC mapping of ours
+  bool peer_sig_opened[mpigx::kMaxRanks] = {};  // peer_sig[q] likewise
+  bool same_device[mpigx::kMaxRanks] = {};      // rank q runs on my GPU (PCI bus/device id)
   mpigx::ShmBlock* shm = nullptr;
   // point-to-point engine (created on first use)
   mpigx::P2PState* p2p = nullptr;

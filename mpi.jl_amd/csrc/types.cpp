@@ -28,6 +28,7 @@
 #include <mutex>
 #include <vector>
 
+#include "handles.hpp"
 #include "launch.hpp"
 #include "runtime.hpp"
 
@@ -35,9 +36,6 @@ using namespace mpigx;
 
 namespace {
 
-constexpr int kDerivedTag = (int)0x8c000000u;  // MPICH HANDLE_KIND_DIRECT | MPID_DATATYPE
-constexpr int kTagMask = (int)0xfc000000u;
-constexpr int kIdxMask = 0x03ffffff;
 constexpr size_t kMaxRuns = 1u << 22;
 
 struct DType {
@@ -59,20 +57,16 @@ struct DType {
 };
 
 std::mutex g_mu;
-std::vector<DType*> g_types;
+// derived types live in libmpigx's own handle space (handles.hpp): an MPICH
+// derived-type handle (0x8c000000 | k) never resolves here
+Registry<DType, HS_DATATYPE> g_types;
 
 DType* lookup(int h) {
-  if ((h & kTagMask) != kDerivedTag) return nullptr;
-  const int i = h & kIdxMask;
-  if (i >= (int)g_types.size() || !g_types[i] || !g_types[i]->live) return nullptr;
-  return g_types[i];
+  DType* t = g_types.get(h);
+  return t && t->live ? t : nullptr;
 }
 
-int new_handle(DType* t) {
-  std::lock_guard<std::mutex> g(g_mu);
-  g_types.push_back(t);
-  return kDerivedTag | (int)(g_types.size() - 1);
-}
+int new_handle(DType* t) { return g_types.add(t); }
 
 int basic_align(int handle, int size) {
   if (handle == MPIGX_C_FLOAT_COMPLEX) return 4;
@@ -441,7 +435,7 @@ int mpigx_type_free(int* datatype) {
     (void)hipFree(d.runs);
     (void)hipFree(d.pfx);
   }
-  g_types[*datatype & kIdxMask] = nullptr;
+  g_types.remove(*datatype);
   delete t;
   *datatype = 0x0c000000;  // MPI_DATATYPE_NULL
   return MPIGX_SUCCESS;

@@ -291,8 +291,9 @@ def main():
     comm = MPI.Init()
     R = Runner(comm)
     phase = os.environ.get("MPIGX_TEST_PHASE", "all")
-    R.golden()
-    R.vgolden()
+    if phase != "oracle":  # MPICH-recorded cases exist for n <= 8
+        R.golden()
+        R.vgolden()
     R.errors()
     R.oracle_cases([("FLOAT", "SUM", 1_000_003), ("DOUBLE", "SUM", 65537), ("FLOAT", "MAX", 100_001),
                     ("INT32_T", "BAND", 262_147), ("INT64_T", "MAX", 50_000), ("BFLOAT16", "SUM", 40_000),

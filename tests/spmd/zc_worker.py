@@ -1,0 +1,138 @@
+"""SPMD worker: the zero-copy Allreduce protocol (mpigx.cpp zc_run).
+
+* steady state: the same (send, recv) pair call after call runs on the cached
+  view — after the first call no host exchange happens at all;
+* a buffer change on ONE rank only aborts the optimistic launch on every
+  rank and repeats it on a fresh view (results still exact);
+* ranks alternating between two buffer pairs in lockstep hit cached views;
+* every result is checked exactly (integer-valued f32: any association
+  gives the same sum), and the per-call host time of the steady state is
+  reported through the raw C ABI (blocking) at 16 / 64 MiB.
+Launched by tests/test_zero_copy_gpu.py.
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (ROOT, os.path.join(ROOT, "mpi.jl_amd")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+import mpigx as MPI  # noqa: E402
+
+
+def stats(L, comm):
+    h, x = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    assert L.mpigx_comm_zc_stats(comm.val, ctypes.byref(h), ctypes.byref(x)) == 0
+    return h.value, x.value
+
+
+def main():
+    comm = MPI.Init()
+    L = MPI.lib()
+    r, n = MPI.Comm_rank(comm), MPI.Comm_size(comm)
+    fails, out = [], {}
+
+    def inputs(count, seed):
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        return [torch.randint(-1000, 1000, (count,), device="cuda", generator=g).float() for _ in range(n)]
+
+    def ar(send, recv):
+        rc = L.mpigx_allreduce(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()), send.numel(),
+                               MPI.FLOAT.val, MPI.SUM.val, comm.val)
+        assert rc == 0, rc
+
+    for mib in (16, 64):
+        count = (mib << 20) // 4
+        xs = inputs(count, 10 + mib)
+        exp = torch.stack(xs).sum(0)
+        send, recv = xs[r].clone(), torch.empty(count, device="cuda")
+        h0, x0 = stats(L, comm)
+        for it in range(12):
+            recv.fill_(-1)
+            ar(send, recv)
+            if not torch.equal(recv, exp):
+                fails.append(("steady", mib, it))
+        h1, x1 = stats(L, comm)
+        # first call: optimistic launch aborts (no view yet), one exchange; then hits only
+        if not (x1 - x0 == 1 and h1 - h0 == 11):
+            fails.append(("steady-stats", mib, h1 - h0, x1 - x0))
+        # host cost of the steady state: wall per blocking call vs device time
+        s = torch.cuda.current_stream()
+        for _ in range(3):
+            ar(send, recv)
+        MPI.Barrier(comm)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        t0 = time.perf_counter()
+        for a, b in ev:
+            a.record(s)
+            ar(send, recv)
+            b.record(s)
+        wall = (time.perf_counter() - t0) / 20
+        torch.cuda.synchronize()
+        dev = sum(a.elapsed_time(b) for a, b in ev) / 20 / 1e3
+        out[f"{mib}MiB"] = {"wall_us": round(wall * 1e6, 2), "device_us": round(dev * 1e6, 2),
+                            "host_overhead_us": round((wall - dev) * 1e6, 2)}
+        # one rank switches its recvbuf: everyone aborts, re-exchanges, exact result
+        if r == n - 1:
+            recv = torch.empty(count + 64, device="cuda")[64:]
+        h2, x2 = stats(L, comm)
+        recv.fill_(-1)
+        ar(send, recv)
+        if not torch.equal(recv, exp):
+            fails.append(("switch-one", mib))
+        h3, x3 = stats(L, comm)
+        if not (x3 - x2 == 1 and h3 - h2 == 0):
+            fails.append(("switch-stats", mib, h3 - h2, x3 - x2))
+        del send, recv, xs, exp
+
+    # lockstep alternation between two buffer pairs: cached views on both
+    count = (16 << 20) // 4
+    xs = inputs(count, 99)
+    exp = torch.stack(xs).sum(0)
+    pairs = [(xs[r].clone(), torch.empty(count, device="cuda")) for _ in range(2)]
+    for it in range(4):  # warm: two exchanges
+        s_, r_ = pairs[it % 2]
+        ar(s_, r_)
+    h0, x0 = stats(L, comm)
+    for it in range(10):
+        s_, r_ = pairs[it % 2]
+        r_.fill_(-1)
+        ar(s_, r_)
+        if not torch.equal(r_, exp):
+            fails.append(("alternate", it))
+    h1, x1 = stats(L, comm)
+    if not (x1 == x0 and h1 - h0 == 10):
+        fails.append(("alternate-stats", h1 - h0, x1 - x0))
+    # in place, and Alltoall through the same protocol
+    buf = xs[r].clone()
+    rc = L.mpigx_allreduce(ctypes.c_void_p(-1 & ((1 << 64) - 1)), ctypes.c_void_p(buf.data_ptr()), count,
+                           MPI.FLOAT.val, MPI.SUM.val, comm.val)
+    if rc != 0 or not torch.equal(buf, exp):
+        fails.append(("inplace", rc))
+    blk = count // n
+    a2s = torch.arange(blk * n, device="cuda", dtype=torch.float32) + 1e6 * r
+    a2r = torch.empty_like(a2s)
+    for it in range(3):
+        a2r.fill_(-1)
+        rc = L.mpigx_alltoall(ctypes.c_void_p(a2s.data_ptr()), blk, MPI.FLOAT.val, ctypes.c_void_p(a2r.data_ptr()),
+                              blk, MPI.FLOAT.val, comm.val)
+        want = torch.cat([torch.arange(r * blk, (r + 1) * blk, device="cuda", dtype=torch.float32) + 1e6 * p
+                          for p in range(n)])
+        if rc != 0 or not torch.equal(a2r, want):
+            fails.append(("alltoall", it, rc))
+    MPI.Barrier(comm)
+    hits, exch = stats(L, comm)
+    MPI.Finalize()
+    print(json.dumps({"rank": r, "n": n, "nfail": len(fails), "failures": [str(f) for f in fails[:20]],
+                      "host_cost": out, "hits": hits, "exchanges": exch}), flush=True)
+    sys.exit(1 if fails else 0)
+
+
+if __name__ == "__main__":
+    main()

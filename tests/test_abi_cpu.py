@@ -120,3 +120,57 @@ def test_python_mirror_datatypes():
     assert D(int).val == C.MPI_INT64_T
     with pytest.raises(TypeError):
         D(str)
+
+
+def test_own_handles_never_alias_mpich():
+    """User ops and derived datatypes live in libmpigx's own handle space
+    (csrc/handles.hpp).  An op or type MPI.jl created in libmpi (MPICH user op
+    0x98000000 | k, derived type 0x8c000000 | k) must be rejected with
+    MPI_ERR_OP / MPI_ERR_TYPE, never resolve to a libmpigx object; a freed
+    handle is rejected even after its slot is reused."""
+    L = mpigx.lib()
+    FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                          ctypes.POINTER(ctypes.c_int))
+    fn = FN(lambda a, b, n, t: None)
+    ops = []
+    for _ in range(3):
+        op = ctypes.c_int()
+        assert L.mpigx_op_create(fn, 0, ctypes.byref(op)) == 0
+        ops.append(op.value)
+    for h in ops:
+        assert h & 0xFC000000 == 0x3C000000 and h & 0xFFFF, hex(h)
+        com = ctypes.c_int(7)
+        assert L.mpigx_op_commutative(h, ctypes.byref(com)) == 0 and com.value == 0
+    com = ctypes.c_int()
+    for k in range(4):  # MPICH direct / indirect user-op handles
+        for foreign in (0x98000000 | k, 0xD8000000 | k):
+            foreign = ctypes.c_int(foreign - (1 << 32)).value
+            assert L.mpigx_op_commutative(foreign, ctypes.byref(com)) == C.MPI_ERR_OP
+            f = ctypes.c_int(foreign)
+            assert L.mpigx_op_free(ctypes.byref(f)) == C.MPI_ERR_OP
+    # free, then reuse the slot: the old handle stays invalid
+    old = ctypes.c_int(ops[0])
+    assert L.mpigx_op_free(ctypes.byref(old)) == 0 and old.value == 0x18000000  # MPI_OP_NULL
+    assert L.mpigx_op_commutative(ops[0], ctypes.byref(com)) == C.MPI_ERR_OP
+    again = ctypes.c_int()
+    assert L.mpigx_op_create(fn, 1, ctypes.byref(again)) == 0
+    assert again.value != ops[0] and again.value & 0xFFFF == ops[0] & 0xFFFF  # same slot, new generation
+    assert L.mpigx_op_commutative(ops[0], ctypes.byref(com)) == C.MPI_ERR_OP
+    for h in (again.value, ops[1], ops[2]):
+        x = ctypes.c_int(h)
+        assert L.mpigx_op_free(ctypes.byref(x)) == 0
+    # derived datatypes
+    t = ctypes.c_int()
+    assert L.mpigx_type_contiguous(4, C.MPI_FLOAT, ctypes.byref(t)) == 0
+    assert t.value & 0xFC000000 == 0x3C000000 and t.value & 0xFFFF
+    assert L.mpigx_type_commit(ctypes.byref(t)) == 0
+    sz = ctypes.c_int()
+    assert L.mpigx_type_size(t.value, ctypes.byref(sz)) == 0 and sz.value == 16
+    for k in range(4):
+        foreign = ctypes.c_int(0x8C000000 | k).value
+        assert L.mpigx_type_size(foreign, ctypes.byref(sz)) == C.MPI_ERR_TYPE
+    # user ops and datatypes are different handle classes
+    assert L.mpigx_op_commutative(t.value, ctypes.byref(com)) == C.MPI_ERR_OP
+    freed = t.value
+    assert L.mpigx_type_free(ctypes.byref(t)) == 0
+    assert L.mpigx_type_size(freed, ctypes.byref(sz)) == C.MPI_ERR_TYPE

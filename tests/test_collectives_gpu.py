@@ -49,3 +49,18 @@ def _summaries(outs):
             if line.startswith("{") and '"checks"' in line:
                 res.append(json.loads(line))
     return res
+
+
+@pytest.mark.parametrize("n", [10, 13])
+def test_oracle_collectives_many_ranks(n):
+    """n = 9..15: pof2 = 8 with up to 7 pre-step partners and n-1 > 8 peers to
+    gather from (NMAX 16 kernels), staged and zero-copy paths, vs the oracle
+    (MPICH recorded fixtures exist for n <= 8 only)."""
+    for extra in ({}, {"MPIGX_ZC_MIN": "1", "MPIGX_ZC_REQUIRE": "1"}):
+        env = dict(ENV, MPIGX_TEST_PHASE="oracle", MPIGX_MAX_BLOCKS="8", **extra)
+        rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "golden_worker.py"), n, timeout=900, extra_env=env)
+        msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
+        assert all(rc == 0 for rc in rcs), msg
+        summ = _summaries(outs)
+        assert len(summ) == n and all(x["nfail"] == 0 and x["checks"] > 50 for x in summ), summ
+

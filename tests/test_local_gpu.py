@@ -69,7 +69,7 @@ def test_all_ops_types(L, dtname, opname):
             assert same_bits(got, expected(ins, dtname, opname, order), dtname == "BFLOAT16"), (n, count, order)
 
 
-@pytest.mark.parametrize("n", [1, 2, 4, 6, 7, 9, 12, 16])
+@pytest.mark.parametrize("n", [1, 2, 4, 6, 7, 8, 9, 12, 13, 15, 16])
 def test_rank_counts(L, n):
     for dtname, opname in (("FLOAT", "SUM"), ("FLOAT", "MAX"), ("INT64_T", "BXOR"), ("DOUBLE", "MIN")):
         for count in (7, 300, 20011):
@@ -77,6 +77,31 @@ def test_rank_counts(L, n):
             for order in (0, 1):
                 got = run_multi(L, ins, dtname, opname, order)
                 assert same_bits(got, expected(ins, dtname, opname, order), dtname == "BFLOAT16"), (dtname, opname, n, count, order)
+
+
+def test_full_shape_multi_vector(L):
+    """The 8-buffer shape (SH_FULL, U vectors per thread): sizes with whole and
+    partial U-blocks, Rabenseifner block boundaries inside a vector (count/8
+    not a multiple of the vector width) and ragged tails, every op family."""
+    for dtname, opname in (("FLOAT", "SUM"), ("FLOAT", "MAX"), ("BFLOAT16", "SUM"), ("BFLOAT16", "MAX"),
+                           ("BFLOAT16", "MIN"), ("DOUBLE", "MIN"), ("INT32_T", "BAND"), ("C_FLOAT_COMPLEX", "PROD")):
+        for count in ((1 << 20) + 13, 3 * 1024 * 8 + 5, 65536):
+            ins = make(dtname, opname, 8, count, 77 + count, edge=True)
+            got = run_multi(L, ins, dtname, opname, 0)
+            assert same_bits(got, expected(ins, dtname, opname, 0), dtname == "BFLOAT16"), (dtname, opname, count)
+
+
+def test_bf16_random_bit_patterns(L):
+    """bf16 definition (fp32 compute, RNE to bf16 after every op, NaN quiet) on
+    uniformly random 16-bit patterns — NaN payloads, infinities, denormals,
+    rounding ties — through the packed pair ops (v_pk_add/mul_f32 +
+    v_cvt_pk_bf16_f32) against the oracle's software rounding."""
+    rng = np.random.default_rng(5)
+    for n in (8, 5):
+        for opname in ("SUM", "PROD", "MAX", "MIN"):
+            ins = [rng.integers(0, 1 << 16, size=(1 << 18) + 3, dtype=np.uint16) for _ in range(n)]
+            got = run_multi(L, ins, "BFLOAT16", opname, 0)
+            assert same_bits(got, expected(ins, "BFLOAT16", opname, 0), True), (n, opname)
 
 
 def test_unaligned_and_empty(L):
