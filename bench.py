@@ -168,20 +168,6 @@ def bench_local(args):
     # association does not depend on count, so a prefix sample is exact
     parity = bool(np.array_equal(out[:k].cpu().numpy().view(np.uint32), ref.view(np.uint32)))
 
-    # copy peak (HBM) on the same device for context
-    src = ins[0]
-    dst = torch.empty_like(src)
-    for _ in range(3):
-        dst.copy_(src)
-    torch.cuda.synchronize()
-    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    c0.record(stream)
-    for _ in range(10):
-        dst.copy_(src)
-    c1.record(stream)
-    torch.cuda.synchronize()
-    copy_gbps = 2 * S * 10 / (c0.elapsed_time(c1) / 1e3) / 1e9
-
     # secondary variants (same kernel family), kernel time only
     def time_variant(dtype_, op):
         xs = [x.to(dtype_) for x in ins] if dtype_ != torch.float32 else ins
@@ -238,7 +224,6 @@ def bench_local(args):
                      "kernel": "fold_local_kernel<OpSum,float,8,TREE>", "kernel_ms": round(kern_ms, 4)},
         "cpu_baseline": cpu,
         "parity_sample_bit_exact": parity,
-        "hbm_copy_peak_GBps_measured": round(copy_gbps, 1),
         "variants": variants,
         "sweep_local_f32_sum": sweep,
         "cpu_reference_allreduce_256MiB": cpu_ar,
@@ -249,9 +234,11 @@ def bench_local(args):
 def bench_allreduce(args):
     import ctypes
 
+    import numpy as np
     import torch
     import torch.distributed as dist
     import mpigx as MPI
+    from oracle import mpich_model as M
 
     rank = int(os.environ.get("RANK", 0))
     n = int(os.environ.get("WORLD_SIZE", 1))
@@ -261,21 +248,26 @@ def bench_allreduce(args):
     comm = MPI.Init()
     dev = torch.device(f"cuda:{local}")
     stream = torch.cuda.current_stream(dev)
+    # same-device ranks (the 1-GPU test box) move HBM bytes through IPC, not xGMI
+    buses = [None] * n
+    dist.all_gather_object(buses, torch.cuda.get_device_properties(dev).pci_bus_id)
+    same_device = len(set(buses)) == 1
 
     def tmax(*xs):
         tt = torch.tensor(list(xs), dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return tt.tolist()
 
-    def time_ar(nbytes, steps, warmup, fn=None):
+    def rank_input(q, count):
+        g = torch.Generator(device=dev).manual_seed(1000 + q)
+        return torch.rand(count, device=dev, generator=g) * 2 - 1
+
+    def time_ar(nbytes, steps, warmup, fn=None, keep=False):
         """(wall s/step, device s/step) of blocking Allreduce!(SUM) f32, max over ranks."""
         count = nbytes // 4
-        g = torch.Generator(device=dev).manual_seed(1000 + rank)
-        send = torch.rand(count, device=dev, generator=g) * 2 - 1
+        send = rank_input(rank, count)
         recv = torch.empty_like(send)
-        call = fn or (lambda: MPI.Allreduce_(send, recv, MPI.SUM, comm))
-        if fn is not None:
-            call = lambda: fn(send, recv)  # noqa: E731
+        call = (lambda: MPI.Allreduce_(send, recv, MPI.SUM, comm)) if fn is None else (lambda: fn(send, recv))
         for _ in range(warmup):
             call()
         torch.cuda.synchronize()
@@ -291,13 +283,37 @@ def bench_allreduce(args):
         dist.barrier()
         wall = (time.perf_counter() - t0) / steps
         kern = sum(a.elapsed_time(b) for a, b in ev) / steps / 1e3
-        return tmax(wall, kern)
+        w, k = tmax(wall, kern)
+        return (w, k, send, recv) if keep else (w, k)
+
+    def check_sample(recv, count, label):
+        """The timed output against the MPICH-pinned oracle on a sample of every
+        rank's (regenerated) random input: the prefix and the elements around
+        every two-shot chunk boundary (each chunk is folded by another rank).
+        The f32 SUM association is element-position independent, so sampled
+        slices are exact.  Max over ranks (every rank checks its recvbuf)."""
+        chunk = -(-(-(-count // n)) // 4) * 4
+        spans = [(0, min(count, 1 << 20))]
+        for c in range(1, n):
+            spans.append((max(0, c * chunk - 4096), min(count, c * chunk + 4096)))
+        spans.append((max(0, count - 4096), count))
+        ok = True
+        xs = [rank_input(q, count) for q in range(n)]
+        for lo, hi in spans:
+            ins = [x[lo:hi].cpu().numpy() for x in xs]
+            ref = M.fold_rsag(ins, "FLOAT", "SUM") if hi - lo >= n else M.allreduce(ins, "FLOAT", "SUM")[0]
+            ok &= bool(np.array_equal(recv[lo:hi].cpu().numpy().view(np.uint32), ref.view(np.uint32)))
+        del xs
+        (bad,) = tmax(0.0 if ok else 1.0)
+        return {"sample_bit_exact_vs_oracle": bad == 0.0, "spans": len(spans), "label": label}
 
     def busbw(nbytes, t):
         return nbytes / t * 2 * (n - 1) / n / 1e9
 
     S = args.mib << 20
-    t, kern = time_ar(S, args.steps, args.warmup)
+    t, kern, send, recv = time_ar(S, args.steps, args.warmup, keep=True)
+    correct = check_sample(recv, S // 4, "timed buffers, default algorithm")
+    del send, recv
 
     # measured xGMI ingress/egress of my GPU over the same workload (SMU
     # metrics, per link, KB; tools/xgmi_counters.py) vs the algorithmic
@@ -309,8 +325,7 @@ def bench_allreduce(args):
     c0 = XC.read(bus)
     if c0 is not None:
         reps = max(args.steps, 10)
-        g = torch.Generator(device=dev).manual_seed(1000 + rank)
-        xs = torch.rand(S // 4, device=dev, generator=g)
+        xs = rank_input(rank, S // 4)
         xr = torch.empty_like(xs)
         dist.barrier()
         for _ in range(reps):
@@ -328,12 +343,6 @@ def bench_allreduce(args):
                   "steps": reps}
         del xs, xr
 
-    # correctness on the timed path: SUM of rank-constant data is exact in f32
-    chk = torch.full((1 << 20,), float(rank + 1), device=dev)
-    out = torch.empty_like(chk)
-    MPI.Allreduce_(chk, out, MPI.SUM, comm)
-    ok = bool(torch.all(out == n * (n + 1) / 2).item())
-
     # measured xGMI: every rank pulls 64 MiB from every peer at once / from one peer
     probe = {}
     for kind, name in ((0, "all_peers"), (1, "one_link")):
@@ -344,41 +353,46 @@ def bench_allreduce(args):
         (sec,) = tmax(secs.value)
         probe[name + "_GBps"] = round(pb * ((n - 1) if kind == 0 else 1) / sec / 1e9, 1)
 
-    # size sweep (mpigx) and the RCCL comparison point (torch.distributed nccl = RCCL)
+    # size sweep (mpigx), algorithm variants, the ring (MPIGX_ALGO=ring, one
+    # ring / every coprime-stride ring) and the RCCL comparison point
     sweep, rccl = {}, {}
-    sizes = [1 << 20, 16 << 20, 64 << 20, S, 1 << 30]
+    sizes = [8 << 10, 1 << 20, 16 << 20, 64 << 20, S, 1 << 30]
     for nb in sizes:
         tw, tk = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
-        sweep[f"{nb >> 20}MiB"] = {"busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1),
-                                   "ms": round(tw * 1e3, 4)}
+        sweep[f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"] = {
+            "busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1), "ms": round(tw * 1e3, 4)}
     for nb in (1 << 20, 16 << 20):
         for algo in ("oneshot", "twoshot"):
             os.environ["MPIGX_ALGO"] = algo
             tw, _ = time_ar(nb, 10, 2)
             sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
         os.environ.pop("MPIGX_ALGO", None)
-    # push two-shot (remote stores into the peers' arenas / recvbufs) vs the
-    # default pull two-shot, with its own exactness check
-    os.environ["MPIGX_ALGO"] = "push"
-    for nb in (16 << 20, S, 1 << 30):
-        tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
-        sweep[f"{nb >> 20}MiB_push"] = round(busbw(nb, tw), 1)
-    big = torch.full((S // 4,), float(rank + 1), device=dev)
-    bout = torch.empty_like(big)
-    MPI.Allreduce_(big, bout, MPI.SUM, comm)
-    (bad,) = tmax(0.0 if bool(torch.all(bout == n * (n + 1) / 2).item()) else 1.0)
-    sweep["push_correct"] = bad == 0.0
-    del big, bout
+    rings = len(M.ring_strides(n, 4))
+    for algo, chans in (("push", 1), ("ring", 1), ("ring", rings)):
+        os.environ["MPIGX_ALGO"] = algo
+        os.environ["MPIGX_RING_CHANNELS"] = str(chans)
+        tag = algo if algo == "push" or chans == 1 else f"ring{chans}"
+        for nb in (16 << 20, S, 1 << 30):
+            tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
+            sweep[f"{nb >> 20}MiB_{tag}"] = round(busbw(nb, tw), 1)
+        # the variant's timed output, checked like the default's
+        _, _, s_, r_ = time_ar(S, 1, 1, keep=True)
+        sweep[f"{tag}_correct"] = check_sample(r_, S // 4, f"{tag} timed buffers")["sample_bit_exact_vs_oracle"] \
+            if algo == "push" else _ring_check(M, np, r_, S // 4, n, rank_input, tmax, chans)
+        del s_, r_
     os.environ.pop("MPIGX_ALGO", None)
+    os.environ.pop("MPIGX_RING_CHANNELS", None)
     if args.no_rccl:
         rccl = {"skipped": True}
+    elif same_device:
+        rccl = {"skipped": "ranks share one GPU (RCCL needs one GPU per rank)"}
     else:
         try:
             ng = dist.new_group(backend="nccl")
             for nb in sizes:
                 tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2,
                                 fn=lambda s_, r_: (r_.copy_(s_), dist.all_reduce(r_, group=ng)))
-                rccl[f"{nb >> 20}MiB"] = round(busbw(nb, tw), 1)
+                rccl[f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"] = round(busbw(nb, tw), 1)
         except Exception as e:  # noqa: BLE001
             rccl = {"error": str(e)[:200]}
 
@@ -416,9 +430,10 @@ def bench_allreduce(args):
             oka = bool(torch.equal(a2r, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) * 100
                                    + rank))
             f = (n - 1) / n
+            (bad,) = tmax(0.0 if (okb and okg and oka) else 1.0)
             cfg4[f"{nb >> 10}KiB"] = {
                 "bcast_busbw": round(nb / tb / 1e9, 2), "allgather_busbw": round(nb / tg / 1e9 * f, 2),
-                "alltoall_busbw": round(nb / ta / 1e9 * f, 2), "ok": okb and okg and oka}
+                "alltoall_busbw": round(nb / ta / 1e9 * f, 2), "ok": bad == 0.0}
             del buf, src, dst, a2s, a2r
 
     # config 5: Scan! / Exscan! / Reduce! with BAND/BOR/MAX on Int32/Int64,
@@ -471,7 +486,18 @@ def bench_allreduce(args):
     ach = busbw(S, kern)
     peak_meas = probe.get("all_peers_GBps")
     peak_nom = XGMI_LINK_GBPS * (n - 1)
-    peak = peak_meas if peak_meas else peak_nom
+    if same_device:
+        roof = {"bound": "hbm (same-device IPC)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                "note": "all ranks share one GPU: peer pulls are HBM reads through IPC mappings, no xGMI"}
+    else:
+        roof = {"bound": "xgmi", "achieved": round(ach, 1), "peak": round(peak_nom, 1), "unit": "GB/s",
+                "frac": round(ach / peak_nom, 4),
+                "traffic": xg["read_bytes_per_step"] if xg else None,
+                "peak_basis": f"nominal {n - 1} links x {XGMI_LINK_GBPS} GB/s per direction (MI355X spec)"}
+    roof.update({"peak_probe_GBps": peak_meas, "frac_vs_probe": round(ach / peak_meas, 4) if peak_meas else None,
+                 "probe_basis": "mpigx_comm_probe: every rank pulling 64 MiB from all peers at once",
+                 "xgmi_traffic": xg})
     if rank == 0:
         res = {
             "metric": "Allreduce! busbw GB/s (256MiB f32 SUM) at 1/2/4/8 GPUs; % of xGMI/HBM peak",
@@ -479,17 +505,13 @@ def bench_allreduce(args):
             "ms_per_step": round(t * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (uniform[-1,1) f32 per rank, seeded, resident in HBM)",
             "config": {"workload": f"config 3 at {args.mib} MiB: MPI.Allreduce!(SUM) f32, blocking, {n} ranks",
-                       "parallelism": f"{n} ranks x 1 GPU (hipIpc peer-mapped HBM over xGMI)",
-                       "bytes_per_rank": S, "algbw_GBps": round(S / t / 1e9, 2)},
-            "roofline": {"bound": "xgmi", "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
-                         "frac": round(ach / peak, 4),
-                         "traffic": xg["read_bytes_per_step"] if xg else None, "xgmi_traffic": xg,
-                         "peak_basis": "measured: every rank pulling from all peers at once (mpigx_comm_probe)"
-                                       if peak_meas else f"nominal {n - 1} x {XGMI_LINK_GBPS} GB/s",
-                         "peak_nominal": peak_nom},
+                       "parallelism": f"{n} ranks x 1 GPU (hipIpc peer-mapped HBM over xGMI)"
+                       if not same_device else f"{n} ranks sharing one GPU (same-device IPC)",
+                       "bytes_per_rank": S, "algbw_GBps": round(S / t / 1e9, 2), "same_device_ranks": same_device},
+            "roofline": roof,
             "cpu_baseline": None,
             "cpu_reference_allreduce": cpu_ar,
-            "correct": ok,
+            "correct": correct,
             "xgmi_probe": probe,
             "sweep_mpigx_busbw": sweep,
             "rccl_busbw": rccl,
@@ -499,6 +521,31 @@ def bench_allreduce(args):
         print(json.dumps(res), flush=True)
     MPI.Finalize()
     dist.destroy_process_group()
+
+
+def _ring_check(M, np, recv, count, n, rank_input, tmax, nch):
+    """The ring's timed output against its own association (oracle fold_ring:
+    chunk c of ring part k is folded along the ring from position c, the
+    running partial as inout) on the first 4096 elements of every chunk of
+    every part.  Max over ranks."""
+    strides = M.ring_strides(n, nch)
+    part = -(-(-(-count // len(strides))) // (n * 4)) * (n * 4)
+    chunk = part // n
+    xs = [rank_input(q, count) for q in range(n)]
+    ok = True
+    for k, st in enumerate(strides):
+        for c in range(n):
+            lo = min(k * part + c * chunk, count)
+            hi = min(lo + 4096, min(k * part + part, count), lo + chunk)
+            if hi <= lo:
+                continue
+            acc = xs[(c * st) % n][lo:hi].cpu().numpy()
+            for i in range(1, n):
+                acc = M.apply_op("SUM", "FLOAT", acc, xs[((c + i) * st) % n][lo:hi].cpu().numpy())
+            ok &= bool(np.array_equal(recv[lo:hi].cpu().numpy().view(np.uint32), acc.view(np.uint32)))
+    del xs
+    (bad,) = tmax(0.0 if ok else 1.0)
+    return bad == 0.0
 
 
 def main():

@@ -64,6 +64,9 @@ enum FoldMode : int {
   M_AR_PUSH = 6,      // push two-shot: write my chunk p into rank p's arena slot [me],
                       // barrier, fold my chunk from my own slots (local HBM), write the
                       // result into every rank's recvbuf (IPC-mapped), barrier
+  M_RED_ZC = 7,       // zero-copy Reduce: barrier, RS of my chunk straight from every
+                      // rank's sendbuf into my arena (the root: its recvbuf), barrier,
+                      // the root gathers every chunk from the arenas, barrier
 };
 
 // Copy-kernel modes (Bcast / Allgather / Alltoall / Barrier).
@@ -74,7 +77,10 @@ enum FoldMode : int {
 enum CopyMode : int {
   C_BCAST = 0, C_ALLGATHER = 1, C_ALLTOALL = 2, C_BARRIER = 3, C_PROBE_ALL = 4, C_PROBE_ONE = 5,
   C_BCAST_SAG = 6,
-  C_ALLTOALL_ZC = 7  // zero-copy: pull block r straight from every rank's (IPC-mapped) sendbuf
+  C_ALLTOALL_ZC = 7,  // zero-copy: pull block r straight from every rank's (IPC-mapped) sendbuf
+  C_ALLGATHER_ZC = 8, // zero-copy: pull block p straight from rank p's sendbuf (or its recvbuf block p)
+  C_BCAST_ZC = 9,     // zero-copy: every non-root pulls the root's buffer
+  C_BCAST_SAG_ZC = 10 // zero-copy scatter + allgather between the user buffers
 };
 
 // Per-call view of the communicator, passed by value to every kernel.
@@ -85,7 +91,7 @@ struct PeerView {
   uint64_t timeout_ticks;      // wall_clock64 ticks (100 MHz) before giving up
   uint64_t* sig[kMaxRanks];    // signal array [kMaxBlocks][kMaxRanks] of every rank
   unsigned* err;               // host-visible error word (0 = ok)
-  unsigned long long* done;    // host-visible completion word (launch sequence), or null
+  unsigned long long* done;    // host-visible completion word (seq << 1 | aborted), or null
   unsigned long long* dcount;  // device-memory block arrival counter (monotone)
   unsigned long long dbase;    // dcount value before this launch
   unsigned long long seq;      // value the last block of this launch stores to *done
@@ -93,7 +99,6 @@ struct PeerView {
   // zero-copy launches (mpigx.cpp zc_run)
   unsigned zc_key;             // id of the buffer-mapping view this launch uses
   int zc_bad;                  // 1: this rank has no valid view (the launch aborts everywhere)
-  unsigned* zc_stale;          // host-visible: set when a zero-copy launch aborted
 };
 
 // Fold-kernel arguments.  Sources/partition are resolved on the host.
@@ -123,6 +128,28 @@ struct FoldArgs {
   void* recv;          // output
   char* zc_recv[kMaxRanks];  // M_AR_ZC / M_AR_PUSH: every rank's recvbuf (IPC-mapped; mine = recv)
   long long slot_bytes;      // M_AR_PUSH: arena bytes per source slot (chunk bytes, 16-B multiple)
+};
+
+// Ring reduce-scatter + allgather (MPIGX_ALGO=ring; kernels.hpp ring_kernel).
+// The message is split into nch contiguous parts, part k travels its own ring
+// of stride stride[k] (coprime with n: 0, s, 2s, ... visits every rank), and
+// each part is cut into n chunks.  Chunk c of a part is folded along its
+// ring starting at the rank in ring position c: partial = OP(partial, x_q),
+// the partial as inout; the block of every rank that owns slice b of channel
+// k synchronises only with block b of its two ring neighbours.
+constexpr int kMaxRings = 4;
+struct RingArgs {
+  PeerView pv;
+  int esize;
+  int nch;                       // rings (channels): blocks b with b % nch == k run ring k
+  int stride[kMaxRings];         // ring k: rank at position i is (i * stride[k]) mod n
+  int pos[kMaxRings];            // my position in ring k
+  long long count;               // elements in this launch (round)
+  long long part;                // elements per ring part (multiple of n*vec)
+  long long chunk;               // elements per chunk of a part (multiple of vec)
+  long long slice;               // elements per block slice of a chunk (multiple of vec)
+  const char* zsend[kMaxRanks];  // every rank's sendbuf (zero-copy view; + round offset)
+  char* zrecv[kMaxRanks];        // every rank's recvbuf (zero-copy view; + round offset)
 };
 
 struct CopyArgs {
@@ -207,10 +234,12 @@ struct ScanArgs {
   PeerView pv;
   int exclusive;
   int esize;
+  int zc;              // 1: operands straight from the peers' sendbufs (src[], zero-copy view)
   long long count;
   long long slice;
   const void* send;
   void* recv;
+  const char* src[kMaxRanks];  // rank q's contribution: its staging arena, or its sendbuf (zc)
 };
 
 }  // namespace mpigx

@@ -8,12 +8,12 @@
 namespace mpigx {
 
 template <int NMAX>
-__device__ __forceinline__ void copy_body(const CopyArgs& A);
+__device__ __forceinline__ int copy_body(const CopyArgs& A);
 
 template <int NMAX>
 __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
-  copy_body<NMAX>(A);
-  signal_done(A.pv);
+  const int ab = copy_body<NMAX>(A);
+  signal_done(A.pv, ab);
 }
 
 // Slice b of chunk k of a chunked byte range: [k*chunk, (k+1)*chunk) ∩ [0,bytes).
@@ -24,13 +24,13 @@ __device__ __forceinline__ void chunk_slice(const CopyArgs& A, int k, int b, lon
 }
 
 template <int NMAX>
-__device__ __forceinline__ void copy_body(const CopyArgs& A) {
+__device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the zero-copy abort verdict
   const PeerView& pv = A.pv;
   const int b = blockIdx.x, r = pv.rank, n = pv.n;
   uint64_t ep = pv.epoch;
   if (A.mode == C_BARRIER) {
     rank_barrier(pv, ep);
-    return;
+    return 0;
   }
   const long long lo = lmin((long long)b * A.slice, A.bytes), hi = lmin(lo + A.slice, A.bytes);
   const long long len = hi - lo;
@@ -42,7 +42,7 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
     // xGMI probe: pull A.bytes from every peer's staging, all peers
     // interleaved (PROBE_ALL: aggregate ingress), or from rank r+1 only
     // (PROBE_ONE: one link); loads folded into a register to stay live.
-    if (!rank_barrier(pv, ep++)) return;
+    if (!rank_barrier(pv, ep++)) return 0;
     const int m = A.mode == C_PROBE_ONE ? 1 : n - 1;
     const long long nv = len / 16;
     u32x4 acc = {0, 0, 0, 0};
@@ -53,16 +53,16 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
     }
     if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u) reinterpret_cast<u32x4*>(mine)[threadIdx.x] = acc;
     rank_barrier(pv, ep++);
-    return;
+    return 0;
   }
   if (A.mode == C_BCAST) {
     // every non-root pulls from the root: the root's egress spreads over
     // its links by itself (one reader per link)
     if (r == A.root) block_copy(mine + lo, send + lo, len);
-    if (!rank_barrier(pv, ep++)) return;
+    if (!rank_barrier(pv, ep++)) return 0;
     if (r != A.root) block_copy(recv + lo, pv.stage[A.root] + lo, len);
     rank_barrier(pv, ep++);
-    return;
+    return 0;
   }
   char* dsts[NMAX];
   const char* srcs[NMAX];
@@ -79,12 +79,12 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
         chunk_slice(A, k, b, &l, &h);
         block_copy(mine + l, send + l, h - l);
       }
-    if (!rank_barrier(pv, ep++)) return;
+    if (!rank_barrier(pv, ep++)) return 0;
     if (r != A.root) {
       chunk_slice(A, r, b, &l, &h);
       block_copy(mine + l, pv.stage[A.root] + l, h - l);
     }
-    if (!rank_barrier(pv, ep++)) return;
+    if (!rank_barrier(pv, ep++)) return 0;
     if (r != A.root) {
       int m = 0;
 #pragma unroll
@@ -104,11 +104,11 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
       block_gather<NMAX>(dsts, srcs, lens, m);
     }
     rank_barrier(pv, ep++);
-    return;
+    return 0;
   }
   if (A.mode == C_ALLGATHER) {
     block_copy(mine + lo, send + lo, len);
-    if (!rank_barrier(pv, ep++)) return;
+    if (!rank_barrier(pv, ep++)) return 0;
     // my own block (unless in place) + every peer's, interleaved
     int m = 0;
 #pragma unroll
@@ -126,12 +126,80 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
     }
     block_gather<NMAX>(dsts, srcs, lens, m);
     rank_barrier(pv, ep++);
-    return;
+    return 0;
+  }
+  if (A.mode == C_ALLGATHER_ZC) {
+    // no staging: block p of my recvbuf <- rank p's block (its sendbuf, or
+    // with IN_PLACE block p of its recvbuf: zsrc[p] points there); every
+    // rank writes only blocks of its own recvbuf other than its own
+    int ab;
+    if (!zc_enter(pv, ep++, &ab)) return 0;
+    if (!ab) {
+      int m = 0;
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j) {
+        dsts[j] = nullptr;
+        srcs[j] = nullptr;
+        lens[j] = 0;
+        if (j < n) {
+          const int p = (r + j) % n;
+          dsts[j] = recv + (long long)p * A.total + lo;
+          srcs[j] = A.zsrc[p] + lo;
+          lens[j] = srcs[j] == dsts[j] ? 0 : len;
+          m = j + 1;
+        }
+      }
+      block_gather<NMAX>(dsts, srcs, lens, m);
+    }
+    rank_barrier(pv, ep++, &ab);
+    return ab;
+  }
+  if (A.mode == C_BCAST_ZC) {
+    // every non-root pulls the root's buffer (its IPC mapping) into its own
+    int ab;
+    if (!zc_enter(pv, ep++, &ab)) return 0;
+    if (!ab && r != A.root) block_copy(recv + lo, A.zsrc[A.root] + lo, len);
+    rank_barrier(pv, ep++, &ab);
+    return ab;
+  }
+  if (A.mode == C_BCAST_SAG_ZC) {
+    // scatter + allgather between the user buffers: rank q pulls chunk q from
+    // the root into its own buffer, then chunk p from rank p's buffer.  Rank
+    // q writes only chunks != q of its buffer after the scatter, and peers
+    // read only its chunk q.
+    long long l, h;
+    int ab;
+    if (!zc_enter(pv, ep++, &ab)) return 0;
+    if (!ab && r != A.root) {
+      chunk_slice(A, r, b, &l, &h);
+      block_copy(recv + l, A.zsrc[A.root] + l, h - l);
+    }
+    if (!rank_barrier(pv, ep++, &ab)) return 0;
+    if (!ab && r != A.root) {
+      int m = 0;
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j) {
+        dsts[j] = nullptr;
+        srcs[j] = nullptr;
+        lens[j] = 0;
+        if (j + 1 < n) {
+          const int p = (r + 1 + j) % n;
+          chunk_slice(A, p, b, &l, &h);
+          dsts[j] = recv + l;
+          srcs[j] = A.zsrc[p] + l;
+          lens[j] = h - l;
+          m = j + 1;
+        }
+      }
+      block_gather<NMAX>(dsts, srcs, lens, m);
+    }
+    rank_barrier(pv, ep++, &ab);
+    return ab;
   }
   if (A.mode == C_ALLTOALL_ZC) {
     // no staging: block r of rank p's sendbuf -> block p of my recvbuf
     int ab;
-    if (!zc_enter(pv, ep++, &ab)) return;  // every rank's sendbuf is ready
+    if (!zc_enter(pv, ep++, &ab)) return 0;  // every rank's sendbuf is ready
     if (!ab) {
     int m = 0;
 #pragma unroll
@@ -150,13 +218,12 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
     block_gather<NMAX>(dsts, srcs, lens, m);
     }
     rank_barrier(pv, ep++, &ab);  // nobody reads my sendbuf any more
-    zc_leave(pv, ab);
-    return;
+    return ab;
   }
   // C_ALLTOALL: block p of my send goes to rank p; block j of my recv comes
   // from rank j's block r.  Staging blocks are A.sstride (16-B multiple) apart.
   for (int p = 0; p < n; ++p) block_copy(mine + (long long)p * A.sstride + lo, send + (long long)p * A.total + lo, len);
-  if (!rank_barrier(pv, ep++)) return;
+  if (!rank_barrier(pv, ep++)) return 0;
   int m = 0;
 #pragma unroll
   for (int j = 0; j < NMAX; ++j) {
@@ -173,6 +240,7 @@ __device__ __forceinline__ void copy_body(const CopyArgs& A) {
   }
   block_gather<NMAX>(dsts, srcs, lens, m);
   rank_barrier(pv, ep++);
+  return 0;
 }
 
 // ---------------------------------------------------------------------------

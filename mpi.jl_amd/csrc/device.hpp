@@ -670,14 +670,13 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
 
 // Zero-copy launches (mpigx.cpp zc_run): entry barrier with the view key and
 // this rank's own verdict (pv.zc_bad: no agreed mapping / a failed import).
+// The launch's abort state (identical in every block of every rank) reaches
+// the host in the completion word itself (kernels.hpp signal_done): ONE store
+// carries both "done" and "aborted", so every rank's host reads the same
+// verdict — a separate flag word raced the completion store over PCIe.
 __device__ __forceinline__ bool zc_enter(const PeerView& pv, uint64_t ep, int* abort) {
   *abort = pv.zc_bad;
   return rank_barrier(pv, ep, abort, pv.zc_key, true);
-}
-// ... and its end: an aborted launch tells the host (which re-resolves).
-__device__ __forceinline__ void zc_leave(const PeerView& pv, int abort) {
-  if (abort && blockIdx.x == 0 && threadIdx.x == 0 && pv.zc_stale)
-    __hip_atomic_store(pv.zc_stale, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace mpigx

@@ -57,6 +57,11 @@ hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs
   return hipGetLastError();
 }
 template <class OP>
+hipError_t ring_op(dim3 grid, hipStream_t s, const RingArgs& a) {
+  hipLaunchKernelGGL((ring_kernel<OP, T>), grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+template <class OP>
 hipError_t scan_op(dim3 grid, hipStream_t s, const ScanArgs& a) {
   hipLaunchKernelGGL((scan_kernel<OP, T>), grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();
@@ -90,6 +95,33 @@ hipError_t MPIGX_CAT(launch_fold_, MPIGX_REP_NAME)(int op, int nmax, int sched, 
       case O_BAND: return fold_op<OpBand>(nmax, sched, grid, s, a);
       case O_BOR: return fold_op<OpBor>(nmax, sched, grid, s, a);
       case O_BXOR: return fold_op<OpBxor>(nmax, sched, grid, s, a);
+      default: break;
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t MPIGX_CAT(launch_ring_, MPIGX_REP_NAME)(int op, dim3 grid, hipStream_t s, const RingArgs& a) {
+  switch (op) {
+    case O_SUM: return ring_op<OpSum>(grid, s, a);
+    case O_PROD: return ring_op<OpProd>(grid, s, a);
+    default: break;
+  }
+  if constexpr (!kCplx) {
+    switch (op) {
+      case O_MIN: return ring_op<OpMin>(grid, s, a);
+      case O_MAX: return ring_op<OpMax>(grid, s, a);
+      case O_LAND: return ring_op<OpLand>(grid, s, a);
+      case O_LOR: return ring_op<OpLor>(grid, s, a);
+      case O_LXOR: return ring_op<OpLxor>(grid, s, a);
+      default: break;
+    }
+  }
+  if constexpr (kInt) {
+    switch (op) {
+      case O_BAND: return ring_op<OpBand>(grid, s, a);
+      case O_BOR: return ring_op<OpBor>(grid, s, a);
+      case O_BXOR: return ring_op<OpBxor>(grid, s, a);
       default: break;
     }
   }

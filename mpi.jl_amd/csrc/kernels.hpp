@@ -27,41 +27,42 @@ __device__ __forceinline__ long long lmin(long long a, long long b) { return a <
 // spins on it instead of paying a hipStreamSynchronize round trip).  One
 // PCIe write per launch: per-block host atomics serialise (128 blocks cost
 // ~65 us, tools/latency.py).
-__device__ __forceinline__ void signal_done(const PeerView& pv) {
+// The stored word is seq << 1 | aborted: a zero-copy launch's abort verdict
+// (the same in every block, device.hpp zc_enter) travels in the completion
+// store itself.
+__device__ __forceinline__ void signal_done(const PeerView& pv, int aborted = 0) {
   if (pv.done) {
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned long long prev =
           __hip_atomic_fetch_add(pv.dcount, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (prev == pv.dbase + gridDim.x - 1)
-        __hip_atomic_store(pv.done, pv.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(pv.done, (pv.seq << 1) | (aborted ? 1ull : 0ull), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
 
 template <class OP, class T, int NMAX, int SCHED>
-__device__ __forceinline__ void fold_body(const FoldArgs& A);
+__device__ __forceinline__ int fold_body(const FoldArgs& A);
 
 template <class OP, class T, int NMAX, int SCHED>
 __global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
-  // The collective modes index FoldArgs with per-rank values.  For float
-  // MIN/MAX and the NMAX-16 kernels the compiler then copied the whole
-  // 840-B argument block to per-thread scratch at entry; those kernels stage
-  // it once per block in LDS instead.  The others (the SUM/NMAX-8 headline
-  // among them) keep reading it from the kernarg segment with scalar loads.
-  if constexpr (NMAX > 8 || role_sensitive<OP, T>::v) {
-    __shared__ FoldArgs sA;
-    static_assert(sizeof(FoldArgs) % 4 == 0, "FoldArgs word copy");
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(&A);
-    uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
-    for (unsigned i = threadIdx.x; i < sizeof(FoldArgs) / 4; i += blockDim.x) d[i] = w[i];
-    __syncthreads();
-    fold_body<OP, T, NMAX, SCHED>(sA);
-    signal_done(sA.pv);
-  } else {
-    fold_body<OP, T, NMAX, SCHED>(A);
-    signal_done(A.pv);
-  }
+  // The collective modes index FoldArgs with per-rank values (peer arenas,
+  // mapped user buffers, fold sources).  Read from the kernarg segment, that
+  // made the compiler copy the whole 864-B argument block to per-thread
+  // scratch at entry in one instantiation family or another as the modes
+  // grew (float MIN/MAX, NMAX 16, then every NMAX-8 kernel once the
+  // zero-copy Reduce joined); every collective fold kernel therefore stages
+  // it once per block in LDS (216 words, one pass of the block).
+  __shared__ FoldArgs sA;
+  static_assert(sizeof(FoldArgs) % 4 == 0, "FoldArgs word copy");
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&A);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
+  for (unsigned i = threadIdx.x; i < sizeof(FoldArgs) / 4; i += blockDim.x) d[i] = w[i];
+  __syncthreads();
+  const int ab = fold_body<OP, T, NMAX, SCHED>(sA);
+  signal_done(sA.pv, ab);
 }
 
 // Config-2 local multi-buffer reduce in a kernel of its own: the collective
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(kThreads) void fold_local_kernel(FoldArgs A) {
 }
 
 template <class OP, class T, int NMAX, int SCHED>
-__device__ __forceinline__ void fold_body(const FoldArgs& A) {
+__device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the zero-copy abort verdict
   const T* const* src = reinterpret_cast<const T* const*>(A.src);
   const T* const* src2 = reinterpret_cast<const T* const*>(A.src2);
   const PeerView& pv = A.pv;
@@ -150,7 +151,7 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     // (skipped everywhere if any rank's view of the mappings is stale)
     const int n = pv.n, r = pv.rank;
     int ab;
-    if (!zc_enter(pv, ep++, &ab)) return;  // every rank's send buffer is ready
+    if (!zc_enter(pv, ep++, &ab)) return 0;  // every rank's send buffer is ready
     if (!ab) {
     const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
     const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
@@ -163,7 +164,7 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
       if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
     fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
     }
-    if (!rank_barrier(pv, ep++, &ab)) return;  // every reduced chunk is in its owner's recvbuf
+    if (!rank_barrier(pv, ep++, &ab)) return 0;  // every reduced chunk is in its owner's recvbuf
     if (!ab) {
     char* dsts[NMAX];
     const char* srcs[NMAX];
@@ -185,8 +186,57 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
     }
     rank_barrier(pv, ep++, &ab);  // nobody reads my buffers any more
-    zc_leave(pv, ab);
-    return;
+    return ab;
+  }
+
+  if (A.mode == M_RED_ZC) {
+    // zero-copy Reduce: RS of my chunk straight from every rank's sendbuf;
+    // non-roots keep it in their arena (slice b at the chunk-relative
+    // offset), the root writes its own chunk into its recvbuf and then
+    // gathers the others' from their arenas
+    const int n = pv.n, r = pv.rank;
+    int ab;
+    if (!zc_enter(pv, ep++, &ab)) return 0;
+    const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+    if (!ab) {
+      bool vec = true;
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s)
+        if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
+#pragma unroll
+      for (int s = 0; s < NMAX / 2; ++s)
+        if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
+      // (two calls, not a select of the output pointer: selecting between
+      // recv and the arena made the compiler copy FoldArgs to scratch)
+      if (r == A.root)
+        fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, vec && recv_vec, tid, nt);
+      else  // arena: element e of my chunk at e - c0 (c0 is a multiple of the vector width)
+        fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, mine - c0, nullptr, vec, tid, nt);
+    }
+    if (!rank_barrier(pv, ep++, &ab)) return 0;
+    if (!ab && r == A.root) {
+      char* dsts[NMAX];
+      const char* srcs[NMAX];
+      long long lens[NMAX];
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j) {
+        dsts[j] = nullptr;
+        srcs[j] = nullptr;
+        lens[j] = 0;
+        if (j + 1 < n) {
+          const int p = (r + 1 + j) % n;
+          const long long d0 = lmin((long long)p * A.chunk, A.count), d1 = lmin(d0 + A.chunk, A.count);
+          const long long l2 = lmin(d0 + (long long)b * A.slice, d1), h2 = lmin(l2 + A.slice, d1);
+          dsts[j] = (char*)(recv + l2);
+          srcs[j] = pv.stage[p] + (l2 - d0) * es;
+          lens[j] = (h2 - l2) * es;
+        }
+      }
+      block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    }
+    rank_barrier(pv, ep++, &ab);  // nobody reads my sendbuf / arena any more
+    return ab;
   }
 
   if (A.mode == M_AR_PUSH) {
@@ -218,7 +268,7 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     // phase 2 writes into the peers' recvbufs through the view's mappings:
     // the barrier checks every rank uses the same view (zc_enter)
     int ab = pv.zc_bad;
-    if (!rank_barrier(pv, ep++, &ab, pv.zc_key, true)) return;
+    if (!rank_barrier(pv, ep++, &ab, pv.zc_key, true)) return 0;
     if (!ab) {
     // phase 2: fold my chunk (slots = local HBM) into my recvbuf, then write
     // the reduced slice into every peer's recvbuf
@@ -248,18 +298,17 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
     }
     rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
-    zc_leave(pv, ab);
-    return;
+    return ab;
   }
 
   if (A.mode == M_AR_ONESHOT || A.mode == M_RED_ONESHOT) {
     const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
     block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);
-    if (!rank_barrier(pv, ep++)) return;
+    if (!rank_barrier(pv, ep++)) return 0;
     if (A.mode == M_AR_ONESHOT || pv.rank == A.root)
       fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
     rank_barrier(pv, ep++);
-    return;
+    return 0;
   }
 
   // two-shot: chunk c = [c*chunk, (c+1)*chunk) ∩ [0,count), block b owns
@@ -270,7 +319,7 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
     block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);
   }
-  if (!rank_barrier(pv, ep++)) return;
+  if (!rank_barrier(pv, ep++)) return 0;
   {
     const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
     const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
@@ -283,7 +332,7 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
       fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, mine, nullptr, true, tid, nt);
   }
   (void)W;
-  if (!rank_barrier(pv, ep++)) return;
+  if (!rank_barrier(pv, ep++)) return 0;
   if (A.mode == M_AR_TWOSHOT || r == A.root) {
     // allgather (or gather at root): every other rank's reduced chunk,
     // all peers interleaved per thread so every link is busy
@@ -307,6 +356,139 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
   }
   rank_barrier(pv, ep++);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Ring reduce-scatter + allgather (RingArgs, common.hpp): the classic
+// bandwidth-optimal schedule the north star names for large messages, here
+// as a comparison against the all-peer direct two-shot.  Per ring every rank
+// pulls from its left neighbour only (one xGMI link per direction per ring;
+// nch rings of distinct strides use nch links).  Per step and block:
+//   wait(left, step-1) -> pull + fold (RS) or pull (AG) -> signal(right)
+// RS step s at ring position p folds chunk (p-s-1): its left neighbour's
+// partial (its send buffer at s = 0) as inout with my contribution; the last
+// RS step writes the final chunk (p+1) into my recvbuf.  AG step t copies
+// chunk (p-t) out of the left neighbour's recvbuf.  Partials of the RS live
+// in the staging arena at the chunk's element offset (one chunk per slot,
+// written once per launch).  Signals are barrier words (device.hpp) stored
+// into the right neighbour's slot [block][me]: monotone epochs, the sticky
+// abort bit of the zero-copy entry.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ring_signal(const PeerView& pv, int to, uint64_t ep, int ab) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab ? 1 : 0) << 24);
+    __hip_atomic_store(pv.sig[to] + (size_t)blockIdx.x * kMaxRanks + pv.rank, word, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+__device__ __forceinline__ bool ring_wait(const PeerView& pv, int from, uint64_t ep) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    const uint64_t* slot = pv.sig[pv.rank] + (size_t)blockIdx.x * kMaxRanks + from;
+    const uint64_t t0 = wall_clock64();
+    int ok = 1;
+    while ((__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> kSigShift) < ep) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > pv.timeout_ticks) {
+        ok = 0;
+        __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// out[i] = OP(acc[i], mine[i]) over [0, len), the block cooperating
+template <class OP, class T>
+__device__ __forceinline__ void ring_fold(T* out, const T* acc, const T* mine, long long len) {
+  constexpr int W = VecW<T>::v;
+  long long i0 = 0;
+  if (((((uintptr_t)out) | ((uintptr_t)acc) | ((uintptr_t)mine)) & 15) == 0) {
+    const long long nv = len / W;
+    for (long long v = threadIdx.x; v < nv; v += blockDim.x) {
+      Vec<T, W> a, b;
+      ldv<T, W>(a, acc + v * W);
+      ldv<T, W>(b, mine + v * W);
+      vapply<OP, T, W>(a, a, b);
+      stv<T, W>(out + v * W, a);
+    }
+    i0 = nv * W;
+  }
+  for (long long i = i0 + threadIdx.x; i < len; i += blockDim.x) out[i] = OP::apply(acc[i], mine[i]);
+}
+
+template <class OP, class T>
+__device__ __forceinline__ int ring_body(const RingArgs& A) {  // returns the abort verdict
+  const PeerView& pv = A.pv;
+  const int n = pv.n, r = pv.rank;
+  const int k = blockIdx.x % A.nch, bc = blockIdx.x / A.nch;
+  const int L = (r - A.stride[k] + n) % n, R = (r + A.stride[k]) % n, pos = A.pos[k];
+  const long long p0 = lmin((long long)k * A.part, A.count), p1 = lmin(p0 + A.part, A.count);
+  auto slice_of = [&](int c, long long* lo, long long* hi) {
+    const long long c0 = lmin(p0 + (long long)c * A.chunk, p1), c1 = lmin(c0 + A.chunk, p1);
+    *lo = lmin(c0 + (long long)bc * A.slice, c1);
+    *hi = lmin(*lo + A.slice, c1);
+  };
+  const T* mine = (const T*)A.zsend[r];
+  T* recv = (T*)A.zrecv[r];
+  uint64_t ep = pv.epoch;
+  int ab;
+  if (!zc_enter(pv, ep++, &ab)) return 0;  // every rank's buffers ready, one view
+  if (!ab) {
+    // reduce-scatter: n-1 steps, forward signals ep .. ep+n-2
+    for (int s = 0; s < n - 1; ++s) {
+      const int c = (pos - s - 1 + 2 * n) % n;
+      long long lo, hi;
+      slice_of(c, &lo, &hi);
+      const T* acc = s == 0 ? (const T*)A.zsend[L] : (const T*)pv.stage[L];
+      T* out = s == n - 2 ? recv : (T*)pv.stage[r];
+      if (s > 0 && !ring_wait(pv, L, ep + s - 1)) return 0;
+      ring_fold<OP, T>(out + lo, acc + lo, mine + lo, hi - lo);
+      ring_signal(pv, R, ep + s, 0);
+      // my left neighbour's chunk `c` of its SEND buffer is read: tell it (with
+      // IN_PLACE its allgather overwrites that chunk of the same buffer)
+      if (s == 0) ring_signal(pv, L, ep, 0);
+    }
+    ep += n - 1;
+    // allgather: n-1 steps, forward signals ep .. ep+n-3 (the last copy feeds nobody)
+    for (int t = 0; t < n - 1; ++t) {
+      if (!ring_wait(pv, L, t == 0 ? ep - 1 : ep + t - 1)) return 0;
+      if (t == 0 && !ring_wait(pv, R, ep - (n - 1))) return 0;  // R read my chunk `pos` (its step 0)
+      const int c = (pos - t + 2 * n) % n;
+      long long lo, hi;
+      slice_of(c, &lo, &hi);
+      block_copy((char*)(recv + lo), (const char*)((const T*)A.zrecv[L] + lo), (hi - lo) * (long long)sizeof(T));
+      if (t < n - 2) ring_signal(pv, R, ep + t, 0);
+    }
+    ep += n - 2;
+  } else {
+    ep += 2 * n - 3;  // every rank aborted at the entry: same epochs, no ring traffic
+  }
+  rank_barrier(pv, ep++, &ab);  // nobody reads my buffers / arena any more
+  return ab;
+}
+
+template <class OP, class T>
+__global__ __launch_bounds__(kThreads) void ring_kernel(RingArgs A) {
+  // per-block ring parameters are indexed by the block's channel: staged in
+  // LDS like FoldArgs (kernarg arrays indexed at run time go to scratch)
+  __shared__ RingArgs sA;
+  static_assert(sizeof(RingArgs) % 4 == 0, "RingArgs word copy");
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&A);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
+  for (unsigned i = threadIdx.x; i < sizeof(RingArgs) / 4; i += blockDim.x) d[i] = w[i];
+  __syncthreads();
+  const int ab = ring_body<OP, T>(sA);
+  signal_done(sA.pv, ab);
 }
 
 // ---------------------------------------------------------------------------
@@ -319,27 +501,28 @@ __device__ __forceinline__ void fold_body(const FoldArgs& A) {
 // owner, in = other half as computed on owner^half).
 // ---------------------------------------------------------------------------
 template <class OP, class T, int SIZE, int W>
-__device__ __forceinline__ void blk_total(const PeerView& pv, int base, int owner, long long e, Vec<T, W>& out) {
+__device__ __forceinline__ void blk_total(const char* const* src, int base, int owner, long long e, Vec<T, W>& out) {
   if constexpr (SIZE == 1) {
-    ldv<T, W>(out, (const T*)pv.stage[base] + e);
+    ldv<T, W>(out, (const T*)src[base] + e);
   } else {
     constexpr int H = SIZE / 2;
     const bool hi_own = (owner - base) & H;
     Vec<T, W> a, c;
-    blk_total<OP, T, H, W>(pv, base, hi_own ? owner ^ H : owner, e, a);       // low half
-    blk_total<OP, T, H, W>(pv, base + H, hi_own ? owner : owner ^ H, e, c);   // high half
+    blk_total<OP, T, H, W>(src, base, hi_own ? owner ^ H : owner, e, a);       // low half
+    blk_total<OP, T, H, W>(src, base + H, hi_own ? owner : owner ^ H, e, c);   // high half
     if (hi_own) vapply<OP, T, W>(out, c, a);
     else vapply<OP, T, W>(out, a, c);
   }
 }
 
 template <class OP, class T, int W>
-__device__ __forceinline__ void blk_total_rt(const PeerView& pv, int m, int base, int owner, long long e, Vec<T, W>& out) {
+__device__ __forceinline__ void blk_total_rt(const char* const* src, int m, int base, int owner, long long e,
+                                             Vec<T, W>& out) {
   switch (m) {
-    case 1: blk_total<OP, T, 1, W>(pv, base, owner, e, out); break;
-    case 2: blk_total<OP, T, 2, W>(pv, base, owner, e, out); break;
-    case 4: blk_total<OP, T, 4, W>(pv, base, owner, e, out); break;
-    default: blk_total<OP, T, 8, W>(pv, base, owner, e, out); break;
+    case 1: blk_total<OP, T, 1, W>(src, base, owner, e, out); break;
+    case 2: blk_total<OP, T, 2, W>(src, base, owner, e, out); break;
+    case 4: blk_total<OP, T, 4, W>(src, base, owner, e, out); break;
+    default: blk_total<OP, T, 8, W>(src, base, owner, e, out); break;
   }
 }
 
@@ -347,12 +530,12 @@ template <class OP, class T, int W>
 __device__ __forceinline__ void scan_at(const ScanArgs& A, long long e, Vec<T, W>& res, bool& have) {
   const int q = A.pv.rank;
   have = !A.exclusive;
-  if (!A.exclusive) ldv<T, W>(res, (const T*)A.pv.stage[q] + e);
+  if (!A.exclusive) ldv<T, W>(res, (const T*)A.src[q] + e);
   for (int m = 1; m < A.pv.n; m <<= 1) {
     if (!(q & m)) continue;
     const int d = q ^ m;
     Vec<T, W> t;
-    blk_total_rt<OP, T, W>(A.pv, m, d & ~(m - 1), d, e, t);
+    blk_total_rt<OP, T, W>(A.src, m, d & ~(m - 1), d, e, t);
     if (!have) {
       res = t;
       have = true;
@@ -363,26 +546,32 @@ __device__ __forceinline__ void scan_at(const ScanArgs& A, long long e, Vec<T, W
 }
 
 template <class OP, class T>
-__device__ __forceinline__ void scan_body(const ScanArgs& A);
+__device__ __forceinline__ int scan_body(const ScanArgs& A);
 
 template <class OP, class T>
 __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs A) {
-  scan_body<OP, T>(A);
-  signal_done(A.pv);
+  const int ab = scan_body<OP, T>(A);
+  signal_done(A.pv, ab);
 }
 
 template <class OP, class T>
-__device__ __forceinline__ void scan_body(const ScanArgs& A) {
+__device__ __forceinline__ int scan_body(const ScanArgs& A) {  // returns the abort verdict
   constexpr int W = VecW<T>::v;
   const PeerView& pv = A.pv;
   const int b = blockIdx.x;
   const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
-  T* mine = (T*)pv.stage[pv.rank];
-  block_copy((char*)(mine + lo), (const char*)A.send + lo * A.esize, (hi - lo) * A.esize);
   uint64_t ep = pv.epoch;
-  if (!rank_barrier(pv, ep++)) return;
+  int ab = 0;
+  if (A.zc) {
+    // zero-copy (out of place only): the operands are the ranks' sendbufs
+    if (!zc_enter(pv, ep++, &ab)) return 0;
+  } else {
+    T* mine = (T*)pv.stage[pv.rank];
+    block_copy((char*)(mine + lo), (const char*)A.send + lo * A.esize, (hi - lo) * A.esize);
+    if (!rank_barrier(pv, ep++)) return 0;
+  }
   T* recv = (T*)A.recv;
-  const bool skip = A.exclusive && pv.rank == 0;  // rank 0's recvbuf untouched
+  const bool skip = ab || (A.exclusive && pv.rank == 0);  // rank 0's Exscan recvbuf untouched
   if (!skip) {
     const long long tid = threadIdx.x, nt = blockDim.x;
     long long s = lo;
@@ -403,7 +592,8 @@ __device__ __forceinline__ void scan_body(const ScanArgs& A) {
       recv[e] = r.x[0];
     }
   }
-  rank_barrier(pv, ep++);
+  rank_barrier(pv, ep++, &ab);
+  return ab;
 }
 
 }  // namespace mpigx

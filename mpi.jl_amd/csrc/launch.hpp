@@ -11,10 +11,12 @@ namespace mpigx {
 using FoldLauncher = hipError_t (*)(int op, int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a);
 using AccLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const AccArgs& a);
 using ScanLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const ScanArgs& a);
+using RingLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const RingArgs& a);
 
 #define MPIGX_DECL_REP(NAME)                                                                     \
   hipError_t launch_fold_##NAME(int op, int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a); \
   hipError_t launch_scan_##NAME(int op, dim3 grid, hipStream_t s, const ScanArgs& a); \
+  hipError_t launch_ring_##NAME(int op, dim3 grid, hipStream_t s, const RingArgs& a); \
   hipError_t launch_acc_##NAME(int op, dim3 grid, hipStream_t s, const AccArgs& a);
 MPIGX_DECL_REP(i8) MPIGX_DECL_REP(u8) MPIGX_DECL_REP(i16) MPIGX_DECL_REP(u16)
 MPIGX_DECL_REP(i32) MPIGX_DECL_REP(u32) MPIGX_DECL_REP(i64) MPIGX_DECL_REP(u64)

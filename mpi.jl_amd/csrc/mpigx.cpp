@@ -124,6 +124,24 @@ FoldLauncher fold_launcher(Rep r) {
     default: return nullptr;
   }
 }
+RingLauncher ring_launcher(Rep r) {
+  switch (r) {
+    case R_I8: return launch_ring_i8;
+    case R_U8: return launch_ring_u8;
+    case R_I16: return launch_ring_i16;
+    case R_U16: return launch_ring_u16;
+    case R_I32: return launch_ring_i32;
+    case R_U32: return launch_ring_u32;
+    case R_I64: return launch_ring_i64;
+    case R_U64: return launch_ring_u64;
+    case R_F32: return launch_ring_f32;
+    case R_F64: return launch_ring_f64;
+    case R_C64: return launch_ring_c64;
+    case R_C128: return launch_ring_c128;
+    case R_BF16: return launch_ring_bf16;
+    default: return nullptr;
+  }
+}
 ScanLauncher scan_launcher(Rep r) {
   switch (r) {
     case R_I8: return launch_scan_i8;
@@ -206,7 +224,6 @@ PeerView make_view(mpigx_comm* c) {
   pv.dcount = c->dcount_dev;
   pv.dbase = c->dcount_total;
   pv.seq = c->launch_seq + 1;
-  pv.zc_stale = c->zc_stale_dev;
   for (int p = 0; p < c->n; ++p) {
     pv.sig[p] = c->peer_sig[p];
     pv.stage[p] = c->peer_stage[p];
@@ -235,20 +252,28 @@ int finish(mpigx_comm* c) {
   if (c->unflagged || c->sync_mode != 1) {
     HIPCK(hipStreamSynchronize(c->stream));
     c->unflagged = false;
+    if (c->sync_mode == 1 && c->launch_seq) {
+      const unsigned long long w = *c->done;  // complete: the last flagged launch's word
+      c->last_aborted = (w >> 1) == c->launch_seq && (w & 1) != 0;
+    }
   } else {
     const double t0 = now_s();
     const double limit = c->timeout_ticks / 1e8 + 5.0;
     unsigned spins = 0;
-    while (*c->done < c->done_target) {
+    unsigned long long w;
+    while (((w = *c->done) >> 1) < c->done_target) {
       // keep point-to-point rendezvous moving while blocked here (a peer may
       // wait on our acknowledgement before it joins this collective)
       if ((spins & 63) == 0) rt::progress_all(c);
       if ((++spins & 1023) == 0 && now_s() - t0 > limit) {
         HIPCK(hipStreamSynchronize(c->stream));
-        c->done_target = *c->done;
+        w = *c->done;
+        c->done_target = w >> 1;
         break;
       }
     }
+    // the last launch's zero-copy verdict (kernels.hpp signal_done)
+    c->last_aborted = (w & 1) != 0;
   }
   if (__atomic_load_n(c->err, __ATOMIC_ACQUIRE) != 0) {
     c->broken = true;
@@ -536,9 +561,9 @@ int zc_exchange(mpigx_comm* c, const void* send, void* recv, ZcLaunch* z) {
 }
 
 bool zc_take_stale(mpigx_comm* c) {
-  if (!__atomic_load_n(c->zc_stale, __ATOMIC_ACQUIRE)) return false;
-  __atomic_store_n(c->zc_stale, 0u, __ATOMIC_RELEASE);
-  return true;
+  const bool a = c->last_aborted;
+  c->last_aborted = false;
+  return a;
 }
 
 // Runs one zero-copy collective: `launch(z)` enqueues its kernel(s) with
@@ -549,7 +574,9 @@ template <class F>
 int zc_run(mpigx_comm* c, const void* send, void* recv, bool* staged, F&& launch) {
   *staged = false;
   ZcLaunch z;
-  if (c->blocking && c->zc_optimistic) {
+  // the optimistic launch needs the abort verdict before returning: blocking
+  // calls completed through the completion word (MPIGX_SYNC_SPIN=1, default)
+  if (c->blocking && c->sync_mode == 1 && c->zc_optimistic) {
     zc_optimistic(c, send, recv, &z);
     int rc = launch(z);
     if (!rc) rc = finish(c);
@@ -568,6 +595,7 @@ int zc_run(mpigx_comm* c, const void* send, void* recv, bool* staged, F&& launch
   int rc = launch(z);
   if (!rc) rc = finish(c);
   if (!rc && zc_take_stale(c)) rc = MPIGX_ERR_INTERN;  // an import failed on some rank
+  if (!rc && z.bad) rc = MPIGX_ERR_INTERN;             // ... here (stream-ordered: known locally)
   return rc;
 }
 
@@ -648,6 +676,72 @@ int allreduce_push(mpigx_comm* c, const ZcLaunch& z, const void* send, long long
   return MPIGX_SUCCESS;
 }
 
+// Ring strides: candidates 1, n-1, 2, n-2, ... coprime with n (each a ring
+// through every rank), distinct, at most `want` (oracle/mpich_model.py
+// ring_strides is the same rule).
+int ring_strides(int n, int want, int* st) {
+  int m = 0;
+  for (int d = 1; d < n && m < want; ++d) {
+    const int cand[2] = {d, n - d};
+    for (int j = 0; j < 2 && m < want; ++j) {
+      int a = cand[j], b = n;
+      while (b) {
+        const int t = a % b;
+        a = b;
+        b = t;
+      }
+      bool dup = false;
+      for (int i = 0; i < m; ++i) dup |= st[i] == cand[j];
+      if (a == 1 && !dup) st[m++] = cand[j];
+    }
+  }
+  return m;
+}
+
+// Ring reduce-scatter + allgather (MPIGX_ALGO=ring, zero-copy mapping of
+// every rank's buffers; kernels.hpp ring_kernel).  MPIGX_RING_CHANNELS rings
+// of distinct strides each carry one contiguous part of the message.  Rounds
+// bound the partials kept in the staging arena (a round's elements in all).
+int allreduce_ring(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeInfo* t, int oc) {
+  const int n = c->n, r = c->rank, es = t->size;
+  const int vec = es >= 16 ? 1 : 16 / es;
+  int want = (int)env_ll("MPIGX_RING_CHANNELS", 1);
+  want = want < 1 ? 1 : want > kMaxRings ? kMaxRings : want;
+  int st[kMaxRings];
+  const int nch = ring_strides(n, want, st);
+  RingLauncher L = ring_launcher(t->rep);
+  long long round = (long long)(c->stage_bytes / es);
+  round = (round / ((long long)nch * n * vec)) * nch * n * vec;
+  for (long long off = 0; off < count; off += round) {
+    const long long cnt = count - off < round ? count - off : round;
+    RingArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    zc_apply(a.pv, z);
+    a.esize = es;
+    a.nch = nch;
+    for (int k = 0; k < nch; ++k) {
+      a.stride[k] = st[k];
+      for (int p = 0; p < n; ++p)
+        if ((long long)p * st[k] % n == r) a.pos[k] = p;
+    }
+    a.count = cnt;
+    a.part = rup(cdiv(cnt, nch), (long long)n * vec);
+    a.chunk = a.part / n;
+    int gc = grid_for(c, a.chunk * es);
+    if (gc * nch > c->max_blocks) gc = c->max_blocks / nch > 0 ? c->max_blocks / nch : 1;
+    a.slice = rup(cdiv(a.chunk, gc), vec);
+    for (int q = 0; q < n; ++q) {
+      a.zsend[q] = z.ps[q] ? z.ps[q] + off * es : nullptr;
+      a.zrecv[q] = z.pr[q] ? z.pr[q] + off * es : nullptr;
+    }
+    HIPCK(L(oc, dim3(gc * nch), c->stream, a));
+    note_launch(c, a.pv, gc * nch);
+    c->epoch += 2 * n - 1;
+  }
+  return MPIGX_SUCCESS;
+}
+
 // Shared driver for Allreduce / Reduce.
 int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, const TypeInfo* t,
                   int oc, int root, bool all) {
@@ -662,12 +756,48 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   if (all && n > 1 && c->zc_min > 0 && count * es >= c->zc_min &&
       !(algo_env && !strcmp(algo_env, "oneshot"))) {
     const bool push = algo_env && !strcmp(algo_env, "push");
+    const bool ring = algo_env && !strcmp(algo_env, "ring");
     bool staged;
     const int rc = zc_run(c, send, recv, &staged, [&](const ZcLaunch& z) {
+      if (ring) return allreduce_ring(c, z, count, t, oc);
       return push ? allreduce_push(c, z, send, count, t, oc) : allreduce_zc(c, z, count, t, oc);
     });
     if (rc || !staged) return rc;
     if (c->zc_require) return MPIGX_ERR_INTERN;  // tests: the path must not fall back
+  }
+  if (!all && n > 1 && c->zc_min > 0 && count * es >= c->zc_min) {
+    // zero-copy Reduce: no copy-in; the reduced chunks wait in the arenas
+    // (rounds of n chunks of at most one arena each) for the root to gather
+    bool staged;
+    const int rc = zc_run(c, send, recv ? recv : (void*)send, &staged, [&](const ZcLaunch& z) {
+      long long zround = (long long)(c->stage_bytes / es) / vec * vec * n;
+      for (long long off = 0; off < count; off += zround) {
+        const long long cnt = count - off < zround ? count - off : zround;
+        FoldArgs a;
+        memset(&a, 0, sizeof a);
+        a.pv = make_view(c);
+        zc_apply(a.pv, z);
+        a.mode = M_RED_ZC;
+        a.esize = es;
+        a.count = cnt;
+        a.gbase = off;
+        a.root = root;
+        a.recv = recv ? (char*)recv + off * es : nullptr;
+        int nmax, sched;
+        const void* ptrs[kMaxRanks];
+        for (int p = 0; p < n; ++p) ptrs[p] = z.ps[p] ? z.ps[p] + off * es : nullptr;
+        plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
+        a.chunk = rup(cdiv(cnt, n), vec);
+        const int grid = grid_for(c, a.chunk * es);
+        a.slice = rup(cdiv(a.chunk, grid), vec);
+        HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
+        note_launch(c, a.pv, grid);
+        c->epoch += 3;
+      }
+      return MPIGX_SUCCESS;
+    });
+    if (rc || !staged) return rc;
+    if (c->zc_require) return MPIGX_ERR_INTERN;
   }
   for (long long off = 0; off < count; off += round) {
     const long long cnt = count - off < round ? count - off : round;
@@ -1025,8 +1155,6 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   HIPCK(hipHostGetDevicePointer((void**)&c->err_dev, c->err, 0));
   c->done = (volatile unsigned long long*)(c->err + 8);  // same pinned page, own 32-B slot
   HIPCK(hipHostGetDevicePointer((void**)&c->done_dev, (void*)c->done, 0));
-  c->zc_stale = c->err + 4;  // byte 16: set by an aborted zero-copy launch
-  HIPCK(hipHostGetDevicePointer((void**)&c->zc_stale_dev, (void*)c->zc_stale, 0));
   c->zc_optimistic = env_ll("MPIGX_ZC_OPTIMISTIC", 1) != 0;
   c->sync_mode = (int)env_ll("MPIGX_SYNC_SPIN", 1);
   HIPCK(hipMalloc((void**)&c->dcount_dev, 64));
@@ -1330,6 +1458,38 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
   bool sag = c->n >= 3 && bytes >= c->bcast_sag_min;
   if (env && !strcmp(env, "direct")) sag = false;
   if (env && !strcmp(env, "sag")) sag = c->n >= 2;
+  if (c->zc_min > 0 && bytes >= c->zc_min) {
+    // zero-copy: the non-roots pull straight from the root's buffer (and, for
+    // scatter + allgather, from each other's), no copy-in at the root
+    bool staged;
+    const int rc = zc_run(c, buf, buf, &staged, [&](const ZcLaunch& z) {
+      CopyArgs a;
+      memset(&a, 0, sizeof a);
+      a.pv = make_view(c);
+      zc_apply(a.pv, z);
+      a.root = root;
+      a.bytes = bytes;
+      a.recv = buf;
+      for (int p = 0; p < c->n; ++p) a.zsrc[p] = z.ps[p];
+      int g;
+      if (sag) {
+        a.mode = C_BCAST_SAG_ZC;
+        a.chunk = rup(cdiv(bytes, c->n), 16);
+        g = grid_for(c, a.chunk);
+        a.slice = rup(cdiv(a.chunk, g), 16);
+      } else {
+        a.mode = C_BCAST_ZC;
+        g = grid_for(c, bytes);
+        a.slice = rup(cdiv(bytes, g), 16);
+      }
+      HIPCK(launch_copy(dim3(g), c->stream, a));
+      note_launch(c, a.pv, g);
+      c->epoch += sag ? 3 : 2;
+      return MPIGX_SUCCESS;
+    });
+    if (rc || !staged) return rc;
+    if (c->zc_require) return MPIGX_ERR_INTERN;
+  }
   for (long long off = 0; off < bytes; off += round) {
     const long long len = bytes - off < round ? bytes - off : round;
     CopyArgs a;
@@ -1393,6 +1553,31 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
       a.total = bytes;
       for (int p = 0; p < n; ++p) a.zsrc[p] = z.ps[p];
       const int g = grid_for(c, bytes * n);
+      a.slice = rup(cdiv(bytes, g), 16);
+      a.send = s;
+      a.recv = recv;
+      HIPCK(launch_copy(dim3(g), c->stream, a));
+      note_launch(c, a.pv, g);
+      c->epoch += 2;
+      return MPIGX_SUCCESS;
+    });
+    if (rc || !staged) return rc;
+    if (c->zc_require) return MPIGX_ERR_INTERN;
+  }
+  if (!alltoall && c->zc_min > 0 && bytes * n >= c->zc_min) {
+    // zero-copy Allgather: block p straight from rank p's sendbuf (IN_PLACE:
+    // from block p of its recvbuf — the registration of `s` points there)
+    bool staged;
+    const int rc = zc_run(c, s, recv, &staged, [&](const ZcLaunch& z) {
+      CopyArgs a;
+      memset(&a, 0, sizeof a);
+      a.pv = make_view(c);
+      zc_apply(a.pv, z);
+      a.mode = C_ALLGATHER_ZC;
+      a.bytes = bytes;
+      a.total = bytes;
+      for (int p = 0; p < n; ++p) a.zsrc[p] = z.ps[p];
+      const int g = grid_for(c, bytes);
       a.slice = rup(cdiv(bytes, g), 16);
       a.send = s;
       a.recv = recv;
@@ -1936,12 +2121,39 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
   }
   ScanLauncher L = scan_launcher(t->rep);
   const int vec = es >= 16 ? 1 : 16 / es;
+  if (sendbuf != MPIGX_IN_PLACE && c->zc_min > 0 && (long long)count * es >= c->zc_min) {
+    // zero-copy (out of place: with IN_PLACE my recvbuf, which I overwrite,
+    // would be the operand the higher ranks read): no copy-in, no rounds
+    bool staged;
+    const int rc = zc_run(c, s, recvbuf, &staged, [&](const ZcLaunch& z) {
+      ScanArgs a;
+      memset(&a, 0, sizeof a);
+      a.pv = make_view(c);
+      zc_apply(a.pv, z);
+      a.zc = 1;
+      a.exclusive = exclusive;
+      a.esize = es;
+      a.count = count;
+      const int g = grid_for(c, (long long)count * es);
+      a.slice = rup(cdiv(count, g), vec);
+      a.send = s;
+      a.recv = recvbuf;
+      for (int p = 0; p < c->n; ++p) a.src[p] = z.ps[p];
+      HIPCK(L(oc, dim3(g), c->stream, a));
+      note_launch(c, a.pv, g);
+      c->epoch += 2;
+      return MPIGX_SUCCESS;
+    });
+    if (rc || !staged) return rc;
+    if (c->zc_require) return MPIGX_ERR_INTERN;
+  }
   long long round = (long long)(c->stage_bytes / es) / vec * vec;
   for (long long off = 0; off < count; off += round) {
     const long long cnt = count - off < round ? count - off : round;
     ScanArgs a;
     memset(&a, 0, sizeof a);
     a.pv = make_view(c);
+    for (int p = 0; p < c->n; ++p) a.src[p] = c->peer_stage[p];
     a.exclusive = exclusive;
     a.esize = es;
     a.count = cnt;

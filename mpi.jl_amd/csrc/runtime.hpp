@@ -168,8 +168,7 @@ struct mpigx_comm {
   std::vector<ZcTuple> ztuples;
   std::vector<ZcView> zviews;
   unsigned zserial = 0, zview_seq = 0;
-  unsigned* zc_stale = nullptr;      // host-pinned word, set by an aborted zero-copy launch
-  unsigned* zc_stale_dev = nullptr;
+  bool last_aborted = false;         // the last completed launch's zero-copy abort verdict
   bool zc_optimistic = true;         // MPIGX_ZC_OPTIMISTIC (blocking calls only)
   unsigned long long zstat_hits = 0, zstat_exchanges = 0;
   std::vector<LocalReg> lreg;

@@ -166,6 +166,93 @@ for (jl, c) in ((:Scan!, :mpigx_scan), (:Exscan!, :mpigx_exscan))
 end
 
 # ---------------------------------------------------------------------------
+# function-valued ops on device buffers: the reference's generic methods
+# (collective.jl:703-705 Allreduce!, :622-625 Reduce!, :770-772 Scan!,
+# :844-846 Exscan!) turn `opfunc` into MPI.Op(opfunc, T) — which for a
+# non-builtin function calls MPI_Op_create in LIBMPI (operators.jl:72-88).  A
+# libmpi op handle means nothing to libmpigx (its own handles live elsewhere,
+# csrc/handles.hpp, and a foreign one is rejected with MPI_ERR_OP), so for
+# ROCBuffers the function goes through device_op: the built-in mapping of
+# operators.jl:39-45 (min/max/+/* on integer and float types, + and * on
+# complex, &/|/⊻ on integers), anything else a libmpigx user op (DeviceOp).
+# ---------------------------------------------------------------------------
+const _MPIInteger = Union{Int8,UInt8,Int16,UInt16,Int32,UInt32,Int64,UInt64}
+const _MPIFloat = Union{Float32,Float64}
+const _MPIComplex = Union{ComplexF32,ComplexF64}
+_is_bf16(::Type{T}) where T = isdefined(Main, :BFloat16s) && T === Main.BFloat16s.BFloat16
+
+builtin_op(f, ::Type{T}) where T = nothing
+for (fn, op, types) in ((min, :MIN, :(Union{_MPIInteger,_MPIFloat})),
+                        (max, :MAX, :(Union{_MPIInteger,_MPIFloat})),
+                        (+, :SUM, :(Union{_MPIInteger,_MPIFloat,_MPIComplex})),
+                        (*, :PROD, :(Union{_MPIInteger,_MPIFloat,_MPIComplex})),
+                        (&, :BAND, :_MPIInteger), (|, :BOR, :_MPIInteger), (⊻, :BXOR, :_MPIInteger))
+    @eval builtin_op(::typeof($fn), ::Type{T}) where {T<:$types} = MPI.$op
+end
+function builtin_op(f, ::Type{T}) where T
+    # bf16 (libmpigx extension): like the float types
+    _is_bf16(T) || return nothing
+    f === min ? MPI.MIN : f === max ? MPI.MAX : f === (+) ? MPI.SUM : f === (*) ? MPI.PROD : nothing
+end
+
+# (op, owned): owned user ops are freed after the call
+function device_op(opfunc, ::Type{T}) where T
+    opfunc isa Op && return (opfunc, false)
+    b = builtin_op(opfunc, T)
+    b !== nothing && return (b, false)
+    (DeviceOp(opfunc, T), true)
+end
+function _with_device_op(f, opfunc, ::Type{T}) where T
+    op, owned = device_op(opfunc, T)
+    try
+        return f(op)
+    finally
+        owned && ccall((:mpigx_op_free, libmpigx), Cint, (Ptr{Cint},), Ref(op.val))
+    end
+end
+
+Allreduce!(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Integer, opfunc, comm::Comm) =
+    _with_device_op(op -> Allreduce!(sendbuf, recvbuf, count, op, comm), opfunc, eltype(recvbuf))
+function Reduce!(sendbuf::DeviceOrSentinel, recvbuf::Union{ROCBuffer,Nothing}, count::Integer, opfunc,
+                 root::Integer, comm::Comm)
+    T = sendbuf isa SentinelPtr ? eltype(recvbuf) : eltype(sendbuf)
+    _with_device_op(op -> Reduce!(sendbuf, recvbuf, count, op, root, comm), opfunc, T)
+end
+Scan!(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Integer, opfunc, comm::Comm) =
+    _with_device_op(op -> Scan!(sendbuf, recvbuf, count, op, comm), opfunc, eltype(recvbuf))
+Exscan!(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Integer, opfunc, comm::Comm) =
+    _with_device_op(op -> Exscan!(sendbuf, recvbuf, count, op, comm), opfunc, eltype(recvbuf))
+# the reference's length-taking and in-place forms (collective.jl:707-714,
+# :626-638, :773-783, :847-857) reach the methods above through dispatch on
+# ROCBuffer; its in-place Scan!/Exscan! forms reference the undefined
+# `sendbuf` (SURVEY §2 reference bugs) — here they work:
+Scan!(buf::ROCBuffer, count::Integer, opfunc, comm::Comm) = Scan!(MPI.IN_PLACE, buf, count, opfunc, comm)
+Scan!(buf::ROCBuffer, opfunc, comm::Comm) = Scan!(MPI.IN_PLACE, buf, length(buf), opfunc, comm)
+Exscan!(buf::ROCBuffer, count::Integer, opfunc, comm::Comm) = Exscan!(MPI.IN_PLACE, buf, count, opfunc, comm)
+Exscan!(buf::ROCBuffer, opfunc, comm::Comm) = Exscan!(MPI.IN_PLACE, buf, length(buf), opfunc, comm)
+
+"""
+    has_rocm()
+
+The ROCm counterpart of `MPI.has_cuda()` (src/environment.jl:308-323), which
+test/test_basic.jl gates the device test mode on: `JULIA_MPI_HAS_ROCM`
+(true/false) overrides; otherwise true when libmpigx loads and a ROCm device
+is visible to it.
+"""
+function has_rocm()
+    flag = get(ENV, "JULIA_MPI_HAS_ROCM", nothing)
+    flag === nothing || return parse(Bool, flag)
+    try
+        p = Ref{Ptr{Cvoid}}(C_NULL)
+        ccall((:mpigx_malloc, libmpigx), Cint, (Ptr{Ptr{Cvoid}}, Csize_t), p, 16) == 0 || return false
+        ccall((:mpigx_free, libmpigx), Cint, (Ptr{Cvoid},), p[])
+        return true
+    catch
+        return false
+    end
+end
+
+# ---------------------------------------------------------------------------
 # point-to-point (src/pointtopoint.jl) on device buffers.  libmpigx requests
 # are MPICH-style Cint handles; they live in their own type so Wait!/Test!
 # dispatch to libmpigx without overwriting MPI.jl's Request methods.
@@ -378,7 +465,7 @@ end
 
 # ---------------------------------------------------------------------------
 # derived datatypes for device buffers (datatypes.jl:62-318, buffers.jl:104-117):
-# libmpigx keeps its own type table (handles in MPICH's derived-type space),
+# libmpigx keeps its own type table (handles in its own space, csrc/handles.hpp),
 # so SubArrays of a ROCBuffer get libmpigx vector / subarray types.
 # ---------------------------------------------------------------------------
 module DevTypes
@@ -447,6 +534,6 @@ end
 # finalizer runs after them (environment.jl:37-62, refcount_inc/_dec).
 atexit(__finalize)
 
-export ROCBuffer, ROCRequest, ROCWin, DeviceOp
+export ROCBuffer, ROCRequest, ROCWin, DeviceOp, has_rocm
 
 end # module

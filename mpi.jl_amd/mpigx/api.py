@@ -450,7 +450,11 @@ def Wtime():
 
 
 def has_rocm():
-    """has_cuda() analogue (environment.jl:308-323): device buffers supported."""
+    """has_cuda() analogue (environment.jl:308-323): device buffers supported.
+    JULIA_MPI_HAS_ROCM=true/false overrides, as JULIA_MPI_HAS_CUDA does there."""
+    flag = os.environ.get("JULIA_MPI_HAS_ROCM")
+    if flag is not None:
+        return flag.strip().lower() in ("true", "1", "yes")
     try:
         lib()
         return _torch().cuda.is_available()

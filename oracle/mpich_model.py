@@ -400,6 +400,78 @@ def fold_linear(inputs, dtname, opname):
     return v
 
 
+def ring_strides(n, want):
+    """Ring strides of mpigx's ring Allreduce (csrc/mpigx.cpp ring_strides):
+    candidates 1, n-1, 2, n-2, ... coprime with n, distinct, at most `want`."""
+    from math import gcd
+    st = []
+    for d in range(1, n):
+        for cand in (d, n - d):
+            if len(st) < want and gcd(cand, n) == 1 and cand not in st:
+                st.append(cand)
+    return st
+
+
+def fold_ring(inputs, dtname, opname, nch=1, round_elems=None):
+    """mpigx ring reduce-scatter + allgather (MPIGX_ALGO=ring; csrc/kernels.hpp
+    ring_body) — an mpigx schedule with no MPICH counterpart.  Per round of
+    ``round_elems`` elements the message is cut into ``nch`` parts of
+    ceil(cnt/nch) elements rounded up to n*vec (vec = 16 B of elements); part k
+    rides the ring of stride s_k, whose position i is rank (i*s_k) mod n, and
+    is cut into n chunks; chunk c is folded left to right along the ring
+    starting at position c, the running partial as inout:
+    ((x_q(c) op x_q(c+1)) op x_q(c+2)) ... op x_q(c+n-1)."""
+    n = len(inputs)
+    count = inputs[0].shape[0]
+    es = _esize(dtname)
+    vec = max(1, 16 // es)
+    strides = ring_strides(n, nch)
+    nch = len(strides)
+    out = np.empty_like(inputs[0])
+    rnd = round_elems or max(count, 1)
+    for off in range(0, count, rnd):
+        cnt = min(rnd, count - off)
+        part = -(-(-(-cnt // nch)) // (n * vec)) * (n * vec)
+        chunk = part // n
+        for k, st in enumerate(strides):
+            p0 = min(k * part, cnt)
+            p1 = min(p0 + part, cnt)
+            for c in range(n):
+                lo = min(p0 + c * chunk, p1)
+                hi = min(lo + chunk, p1)
+                if lo == hi:
+                    continue
+                acc = inputs[(c * st) % n][off + lo:off + hi].copy()
+                for i in range(1, n):
+                    acc = apply_op(opname, dtname, acc, inputs[((c + i) * st) % n][off + lo:off + hi])
+                out[off + lo:off + hi] = acc
+    return out
+
+
+def ring_round_elems(stage_bytes, n, dtname, nch=1):
+    """Elements per round of the ring (mpigx.cpp allreduce_ring): the staging
+    arena (rounded up to 4 KiB) in elements, a multiple of nch*n*vec."""
+    es = _esize(dtname)
+    vec = max(1, 16 // es)
+    nch = len(ring_strides(n, nch))
+    sb = (stage_bytes + 4095) // 4096 * 4096
+    q = nch * n * vec
+    return (sb // es) // q * q
+
+
+def sum_tolerance(inputs, dtname):
+    """|a - b| bound between two summation orders of the same n values
+    (2 (n-1) u sum|x|, u = unit roundoff): the stated tolerance of the ring's
+    float SUM against MPICH's pairwise tree."""
+    n = len(inputs)
+    u = {"FLOAT": 2.0 ** -24, "DOUBLE": 2.0 ** -53, "BFLOAT16": 2.0 ** -8}[dtname]
+    if dtname == "BFLOAT16":
+        mag = sum(np.abs(bf16_to_f32(x).astype(np.float64)) for x in inputs)
+    else:
+        mag = sum(np.abs(x.astype(np.float64)) for x in inputs)
+    return 2 * (n - 1) * u * mag
+
+
 def fold_tree(inputs, dtname, opname):
     """MPICH single-node Allreduce result (binomial tree to rank 0, <= 2 KiB regime)."""
     return reduce(list(inputs), dtname, opname, 0, short_msg=1 << 62)

@@ -264,6 +264,35 @@ class Runner:
             got = self.run("bcast", ins1, "UINT8_T", None, count, root=1 % n)
             self.check(same_bits(got, ins1[1 % n]), ("bcast-u8", count))
 
+    def ring_cases(self, nchs=(1, 2, 4)):
+        """MPIGX_ALGO=ring (zero-copy path): bit-exact against the ring's own
+        association (oracle fold_ring, rounds included), and against MPICH:
+        integer / bitwise ops exact, float SUM within the stated tolerance
+        2(n-1) u sum|x| (oracle sum_tolerance)."""
+        n, r = self.n, self.r
+        stage = int(os.environ.get("MPIGX_STAGING_BYTES", 512 << 20))
+        cases = (("FLOAT", "SUM", 1_000_003), ("DOUBLE", "SUM", 65537), ("FLOAT", "MAX", 100_001),
+                 ("INT32_T", "BAND", 262_147), ("INT64_T", "SUM", 50_000), ("BFLOAT16", "SUM", 40_000),
+                 ("C_FLOAT_COMPLEX", "PROD", 3333), ("UINT8_T", "BXOR", 100_000), ("FLOAT", "SUM", 5))
+        os.environ["MPIGX_ALGO"] = "ring"
+        for nch in nchs:
+            os.environ["MPIGX_RING_CHANNELS"] = str(nch)
+            for i, (dt, op, count) in enumerate(cases):
+                ins = make(dt, op, n, count, 3000 + i, edge=op in ("MAX", "MIN"))
+                exp = M.fold_ring(ins, dt, op, nch, M.ring_round_elems(stage, n, dt, nch))
+                for inplace in (False, True):
+                    got = self.run("allreduce", ins, dt, op, count, inplace=inplace)
+                    self.check(same_bits(got, exp, dt == "BFLOAT16"), ("ring", nch, dt, op, count, inplace))
+                kind = M.DTYPES[dt][2]
+                mp = M.allreduce(ins, dt, op)[0]
+                if kind in ("int", "uint", "byte"):
+                    self.check(np.array_equal(exp, mp), ("ring-vs-mpich", dt, op))
+                elif dt in ("FLOAT", "DOUBLE") and op == "SUM":
+                    err = np.abs(exp.astype(np.float64) - mp.astype(np.float64))
+                    self.check(bool((err <= M.sum_tolerance(ins, dt)).all()), ("ring-tolerance", dt, count))
+        os.environ.pop("MPIGX_ALGO", None)
+        os.environ.pop("MPIGX_RING_CHANNELS", None)
+
     def linear_order(self):
         MPI.set_reduce_order(self.comm, 1)
         for i, (dtname, opname, count) in enumerate((("FLOAT", "SUM", 5000), ("DOUBLE", "SUM", 70001),
@@ -299,12 +328,17 @@ def main():
                     ("INT32_T", "BAND", 262_147), ("INT64_T", "MAX", 50_000), ("BFLOAT16", "SUM", 40_000),
                     ("C_FLOAT_COMPLEX", "PROD", 3333), ("UINT8_T", "BXOR", 100_000)])
     R.linear_order()
+    zc = bool(os.environ.get("MPIGX_ZC_MIN"))
+    if zc:
+        R.ring_cases()
     if phase == "all":
         # rounds: a communicator whose staging arena is 1 MiB forces multi-round launches
         os.environ["MPIGX_STAGING_BYTES"] = str(1 << 20)
         c2 = MPI.Comm_dup(comm)
         R2 = Runner(c2)
         R2.oracle_cases([("FLOAT", "SUM", 700_001), ("DOUBLE", "MIN", 300_001)])
+        if zc:
+            R2.ring_cases(nchs=(1, 2))
         MPI.free(c2)
         R.fail += R2.fail
         R.ran += R2.ran

@@ -1,0 +1,139 @@
+"""SPMD worker: parity at the headline sizes (BASELINE configs 3-5) on the
+DEFAULT paths (the algorithm the size selects — zero-copy at these sizes):
+
+* Allreduce! 256 MiB f32 SUM: bit-exact against the oracle (fold_rsag, the
+  MPICH Rabenseifner association) on sampled slices spanning every two-shot
+  chunk boundary, the prefix and the tail;
+* Bcast! / Allgather! / Alltoall! at 512 MiB: exact (torch.equal) against
+  the regenerated inputs;
+* Scan! / Exscan! / Reduce! on 64 Mi Int32 / Int64 elements with BAND / BOR /
+  MAX: exact against the prefix folds of the regenerated inputs (integer ops
+  are association-free).
+Every rank regenerates every rank's seeded input on its own device.
+Launched by tests/test_headline_gpu.py.
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (ROOT, os.path.join(ROOT, "mpi.jl_amd")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mpigx as MPI  # noqa: E402
+from oracle import mpich_model as M  # noqa: E402
+
+
+def main():
+    comm = MPI.Init()
+    r, n = MPI.Comm_rank(comm), MPI.Comm_size(comm)
+    dev = torch.device("cuda")
+    fails = []
+
+    def f32_input(q, count, seed):
+        g = torch.Generator(device=dev).manual_seed(seed + q)
+        return torch.rand(count, device=dev, generator=g) * 2 - 1
+
+    # --- Allreduce 256 MiB f32 SUM, default path
+    count = (256 << 20) // 4
+    send = f32_input(r, count, 1000)
+    recv = torch.empty_like(send)
+    MPI.Allreduce_(send, recv, MPI.SUM, comm)
+    xs = [f32_input(q, count, 1000) for q in range(n)]
+    chunk = -(-(-(-count // n)) // 4) * 4
+    spans = [(0, 1 << 16), (count - (1 << 16), count)] + \
+            [(c * chunk - 4096, c * chunk + 4096) for c in range(1, n)] + \
+            [(count // 8 * k - 2048, count // 8 * k + 2048) for k in range(1, 8)]  # Rabenseifner blocks
+    for lo, hi in spans:
+        ins = [x[lo:hi].cpu().numpy() for x in xs]
+        ref = M.fold_rsag(ins, "FLOAT", "SUM")
+        if not np.array_equal(recv[lo:hi].cpu().numpy().view(np.uint32), ref.view(np.uint32)):
+            fails.append(("allreduce-256MiB", lo, hi))
+    # the same call again (cached zero-copy view) gives the same bits
+    again = torch.empty_like(send)
+    MPI.Allreduce_(send, again, MPI.SUM, comm)
+    if not torch.equal(again.view(torch.int32), recv.view(torch.int32)):
+        fails.append(("allreduce-repeat",))
+    del send, recv, again, xs
+
+    # --- Bcast / Allgather / Alltoall at 512 MiB
+    nb = 512 << 20
+    cnt = nb // 4
+    for root in sorted({0, n - 1}):
+        buf = f32_input(r, cnt, 2000) if r == root else torch.zeros(cnt, device=dev)
+        MPI.Bcast_(buf, root, comm)
+        if not torch.equal(buf, f32_input(root, cnt, 2000)):
+            fails.append(("bcast-512MiB", root))
+        del buf
+    per = cnt // n
+    src = f32_input(r, per, 3000)
+    dst = torch.empty(per * n, device=dev)
+    MPI.Allgather_(src, dst, per, comm)
+    for q in range(n):
+        if not torch.equal(dst[q * per:(q + 1) * per], f32_input(q, per, 3000)):
+            fails.append(("allgather-512MiB", q))
+    # in place
+    dst.zero_()
+    dst[r * per:(r + 1) * per] = src
+    MPI.Allgather_(dst, per, comm)
+    for q in range(n):
+        if not torch.equal(dst[q * per:(q + 1) * per], f32_input(q, per, 3000)):
+            fails.append(("allgather-inplace-512MiB", q))
+    del src, dst
+    a2s = f32_input(r, per * n, 4000)
+    a2r = torch.empty_like(a2s)
+    MPI.Alltoall_(a2s, a2r, per, comm)
+    for q in range(n):
+        if not torch.equal(a2r[q * per:(q + 1) * per], f32_input(q, per * n, 4000)[r * per:(r + 1) * per]):
+            fails.append(("alltoall-512MiB", q))
+    del a2s, a2r
+
+    # --- Scan / Exscan / Reduce, 64 Mi elements of Int32 / Int64
+    ops = (("BAND", MPI.BAND, torch.bitwise_and), ("BOR", MPI.BOR, torch.bitwise_or), ("MAX", MPI.MAX, torch.maximum))
+    cnt = 64 << 20
+    for tdt, lim in ((torch.int32, 1 << 31), (torch.int64, 1 << 62)):
+        def gen(q):
+            g = torch.Generator(device=dev).manual_seed(7000 + 31 * q)
+            return torch.randint(-lim, lim, (cnt,), dtype=tdt, device=dev, generator=g)
+        mine = gen(r)
+        for oname, op, fn in ops:
+            pref = None
+            for q in range(r + 1):  # prefix through my rank
+                pref = gen(q) if pref is None else fn(pref, gen(q))
+            out = torch.zeros_like(mine)
+            MPI.Scan_(mine, out, op, comm)
+            if not torch.equal(out, pref):
+                fails.append(("scan", str(tdt), oname))
+            out.fill_(7)
+            MPI.Exscan_(mine, out, op, comm)
+            if r > 0:
+                ex = None
+                for q in range(r):
+                    ex = gen(q) if ex is None else fn(ex, gen(q))
+                if not torch.equal(out, ex):
+                    fails.append(("exscan", str(tdt), oname))
+            elif not bool((out == 7).all()):
+                fails.append(("exscan-rank0-touched", str(tdt), oname))
+            root = n - 1
+            rout = torch.zeros_like(mine) if r == root else None
+            MPI.Reduce_(mine, rout, op, root, comm)
+            if r == root:
+                tot = pref
+                for q in range(r + 1, n):
+                    tot = fn(tot, gen(q))
+                if not torch.equal(rout, tot):
+                    fails.append(("reduce", str(tdt), oname))
+            del out, rout, pref
+        del mine
+    MPI.Barrier(comm)
+    MPI.Finalize()
+    print(json.dumps({"rank": r, "n": n, "nfail": len(fails), "failures": [str(f) for f in fails[:20]]}), flush=True)
+    sys.exit(1 if fails else 0)
+
+
+if __name__ == "__main__":
+    main()

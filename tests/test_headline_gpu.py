@@ -1,0 +1,23 @@
+"""Parity at BASELINE's headline sizes on the default (size-selected,
+zero-copy) paths — 256 MiB Allreduce, 512 MiB Bcast/Allgather/Alltoall,
+64 Mi-element integer Scan/Exscan/Reduce (tests/spmd/headline_worker.py) — at
+n = 2 and 4 ranks sharing the one GPU of the test box."""
+import json
+import os
+
+import pytest
+
+from spmd_launch import ROOT, launch
+
+pytestmark = pytest.mark.gpu
+
+ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_MAX_BLOCKS": "32", "MPIGX_TIMEOUT_MS": "60000"}
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_headline_sizes(n):
+    rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "headline_worker.py"), n, timeout=900, extra_env=ENV)
+    msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
+    assert all(rc == 0 for rc in rcs), msg
+    res = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"nfail"' in l]
+    assert len(res) == n and all(x["nfail"] == 0 for x in res), res

@@ -53,3 +53,7 @@ def test_hot_fold_kernels_have_no_scratch(obj, tmp_path):
     coll = {k: v for k, v in sizes.items() if "11fold_kernel" in k}
     assert coll, f"no fold_kernel in {obj}"
     assert all(v == 0 for v in coll.values()), {k: v for k, v in coll.items() if v}
+    # ring reduce-scatter + allgather and Scan / Exscan likewise
+    other = {k: v for k, v in sizes.items() if "11ring_kernel" in k or "11scan_kernel" in k}
+    assert other, f"no ring/scan kernel in {obj}"
+    assert all(v == 0 for v in other.values()), {k: v for k, v in other.items() if v}

@@ -127,3 +127,83 @@ def test_bf16_rounding_definition():
     back = M.bf16_to_f32(b)
     assert back[0] == 1.0 and back[1] == 1.0 and back[2] == 1.015625 and back[3] == -2.5
     assert np.isinf(back[4]) and np.isnan(back[5])
+
+
+def _ring_step_simulation(inputs, dtname, opname, nch, round_elems):
+    """The ring schedule of csrc/kernels.hpp ring_body played out message by
+    message (per ring, per step: position p folds chunk p-s-1 with the left
+    neighbour's partial as inout, then the allgather hands final chunks right)."""
+    n = len(inputs)
+    count = inputs[0].shape[0]
+    vec = max(1, 16 // np.dtype(M.DTYPES[dtname][1]).itemsize)
+    strides = M.ring_strides(n, nch)
+    recv = [np.empty_like(inputs[0]) for _ in range(n)]
+    for off in range(0, count, round_elems):
+        cnt = min(round_elems, count - off)
+        part = -(-(-(-cnt // len(strides))) // (n * vec)) * (n * vec)
+        chunk = part // n
+        for k, st in enumerate(strides):
+            p0, p1 = min(k * part, cnt), min(k * part + part, cnt)
+            rank_at = [(i * st) % n for i in range(n)]
+
+            def sl(c):
+                lo = min(p0 + c * chunk, p1)
+                return slice(off + lo, off + min(lo + chunk, p1))
+            stage = [dict() for _ in range(n)]
+            for s in range(n - 1):
+                new = [dict() for _ in range(n)]
+                for pos in range(n):
+                    q, left = rank_at[pos], rank_at[(pos - 1) % n]
+                    c = (pos - s - 1) % n
+                    acc = inputs[left][sl(c)] if s == 0 else stage[left][c]
+                    val = M.apply_op(opname, dtname, acc, inputs[q][sl(c)])
+                    if s == n - 2:
+                        recv[q][sl(c)] = val
+                    else:
+                        new[q][c] = val
+                stage = new
+            for t in range(n - 1):
+                snap = [x.copy() for x in recv]
+                for pos in range(n):
+                    q, left = rank_at[pos], rank_at[(pos - 1) % n]
+                    c = (pos - t) % n
+                    recv[q][sl(c)] = snap[left][sl(c)]
+    return recv
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_ring_oracle_matches_step_simulation(n):
+    """oracle fold_ring (the association the ring kernel is checked against on
+    the GPU) equals the ring schedule simulated step by step, on every rank;
+    integer results equal MPICH's; float SUM stays within sum_tolerance of
+    MPICH's pairwise tree."""
+    rng = np.random.default_rng(n)
+    for dt, op, count in (("FLOAT", "SUM", 1000), ("FLOAT", "MAX", 333), ("INT32_T", "SUM", 517),
+                          ("BFLOAT16", "SUM", 999), ("DOUBLE", "SUM", 64)):
+        if dt == "BFLOAT16":
+            ins = [M.f32_to_bf16(rng.uniform(-1, 1, count).astype(np.float32)) for _ in range(n)]
+        elif dt == "INT32_T":
+            ins = [rng.integers(-2**31, 2**31, count, dtype=np.int64).astype(np.int32) for _ in range(n)]
+        else:
+            ins = [rng.uniform(-1, 1, count).astype(M.DTYPES[dt][1]) for _ in range(n)]
+        for nch in (1, 2, 4):
+            for rnd in (count, 16 * n * 4):
+                sim = _ring_step_simulation(ins, dt, op, nch, rnd)
+                exp = M.fold_ring(ins, dt, op, nch, rnd)
+                for q in range(n):
+                    assert same_bits(sim[q], exp, dt == "BFLOAT16"), (dt, op, nch, rnd, q)
+        mp = M.allreduce(ins, dt, op)[0]
+        if dt == "INT32_T":
+            assert np.array_equal(M.fold_ring(ins, dt, op), mp)
+        if dt in ("FLOAT", "DOUBLE") and op == "SUM":
+            err = np.abs(M.fold_ring(ins, dt, op).astype(np.float64) - mp.astype(np.float64))
+            assert (err <= M.sum_tolerance(ins, dt)).all()
+
+
+def test_ring_strides():
+    assert M.ring_strides(8, 4) == [1, 7, 3, 5]
+    assert M.ring_strides(2, 4) == [1]
+    assert M.ring_strides(6, 4) == [1, 5]
+    for n in range(2, 17):
+        for st in M.ring_strides(n, 4):
+            assert sorted((i * st) % n for i in range(n)) == list(range(n))
