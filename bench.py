@@ -221,7 +221,10 @@ def bench_local(args):
                    "algorithmic_bytes_per_step": algo},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": "fold_local_kernel<OpSum,float,8,TREE>", "kernel_ms": round(kern_ms, 4)},
+                     "kernel": "fold_local_kernel<OpSum,float,NMAX 8,TREE,SH_FULL,U 4>", "kernel_ms": round(kern_ms, 4),
+                     "achieved_basis": "9 x 256 MiB algorithmic bytes / HIP-event time per launch on the launch stream",
+                     "traffic_basis": "rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE per dispatch (gfx950 FETCH_SIZE "
+                                      "halving, MI355X_MICROARCH.md), profiles/r02_traffic.json"},
         "cpu_baseline": cpu,
         "parity_sample_bit_exact": parity,
         "variants": variants,

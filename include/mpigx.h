@@ -142,6 +142,9 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
  * host exchanges of buffer registrations there were.  Diagnostic. */
 int mpigx_comm_zc_stats(mpigx_comm_t comm, unsigned long long *optimistic_hits,
                         unsigned long long *exchanges);
+/* Host time of the last collective call from its entry to its first kernel
+ * launch (argument checks, planning, zero-copy view resolution).  Diagnostic. */
+int mpigx_comm_host_stats(mpigx_comm_t comm, double *prelaunch_us);
 
 /* Diagnostic (bench roofline denominator): every rank pulls `bytes` from
  * every peer's staging arena at once (kind 0: aggregate xGMI ingress) or

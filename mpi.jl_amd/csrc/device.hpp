@@ -301,6 +301,23 @@ __device__ __forceinline__ void stv(T* p, const Vec<T, W>& d) {
   }
 }
 
+// Write-through (sc1) 16-B stores: the line leaves the XCD's L2 with the
+// store instead of staying dirty there until an eviction interleaves its
+// write-back with the read streams.  Config-2 fold output only (nobody reads
+// it back soon): 8 x 256 MiB f32 SUM 387 -> 380 us on the same box
+// (tools/fold_tune.hip, profiles/r02_fold_tune_placement.json; nt stores
+// 400 us).  A buffer store with cache bits (aux 16 = sc1), so the compiler
+// owns the data-register hazard an inline-asm store would leave open; the
+// descriptor is built per block span from wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+}
+template <class T, int W>
+__device__ __forceinline__ void stv_wt(__amdgpu_buffer_rsrc_t r, int byte_off, const Vec<T, W>& d) {
+  static_assert(W * sizeof(T) == 16, "16-B vectors only");
+  __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(d.x), r, byte_off, 0, 16);
+}
+
 // d = OP(a, b) element-wise, a = inout (d may alias a or b)
 template <class OP, class T, int W>
 __device__ __forceinline__ void vapply(Vec<T, W>& d, const Vec<T, W>& a, const Vec<T, W>& b) {

@@ -103,12 +103,14 @@ __global__ __launch_bounds__(kThreads) void fold_local_kernel(FoldArgs A) {
       Leaves<T, NMAX, SHAPE, W> L[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) load_leaves<T, NMAX, SCHED, SHAPE, W>(A, src, src2, (v0 + u * kThreads) * W, L[u]);
+      // the block's output span (U * kThreads vectors), write-through stores
+      const __amdgpu_buffer_rsrc_t span = span_rsrc(out + (v0 - tid) * W, U * kThreads * 16);
       unsigned strad = 0;  // vectors straddling a Rabenseifner block boundary
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long long e = (v0 + u * kThreads) * W;
         Vec<T, W> r;
-        if (fold_leaves<OP, T, NMAX, SCHED, SHAPE, W>(A, e, L[u], r)) stv<T, W>(out + e, r);
+        if (fold_leaves<OP, T, NMAX, SCHED, SHAPE, W>(A, e, L[u], r)) stv_wt<T, W>(span, (int)(tid + u * kThreads) * 16, r);
         else strad |= 1u << u;
       }
 #pragma unroll 1

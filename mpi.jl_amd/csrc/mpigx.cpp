@@ -233,6 +233,10 @@ PeerView make_view(mpigx_comm* c) {
 
 // Account for one launch of `grid` blocks made with view `pv`.
 void note_launch(mpigx_comm* c, const PeerView& pv, unsigned grid) {
+  if (c->launch_pending) {
+    c->last_prelaunch_s = now_s() - c->t_entry;
+    c->launch_pending = false;
+  }
   if (pv.done) {
     c->dcount_total += grid;
     c->launch_seq += 1;
@@ -840,6 +844,8 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
 int check_comm(mpigx_comm* c) {
   if (!c) return MPIGX_ERR_COMM;
   if (c->broken) return MPIGX_ERR_OTHER;
+  c->t_entry = now_s();  // host-cost diagnostic (mpigx_comm_host_stats)
+  c->launch_pending = true;
   if (hipSetDevice(c->device) != hipSuccess) return MPIGX_ERR_INTERN;
   return MPIGX_SUCCESS;
 }
@@ -1385,6 +1391,11 @@ int mpigx_comm_zc_stats(mpigx_comm_t c, unsigned long long* optimistic_hits, uns
   if (!c) return MPIGX_ERR_COMM;
   if (optimistic_hits) *optimistic_hits = c->zstat_hits;
   if (exchanges) *exchanges = c->zstat_exchanges;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_host_stats(mpigx_comm_t c, double* prelaunch_us) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (prelaunch_us) *prelaunch_us = c->last_prelaunch_s * 1e6;
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_set_reduce_order(mpigx_comm_t c, int order) {

@@ -169,6 +169,8 @@ struct mpigx_comm {
   std::vector<ZcView> zviews;
   unsigned zserial = 0, zview_seq = 0;
   bool last_aborted = false;         // the last completed launch's zero-copy abort verdict
+  double t_entry = 0, last_prelaunch_s = 0;  // host time from API entry to the first launch
+  bool launch_pending = false;
   bool zc_optimistic = true;         // MPIGX_ZC_OPTIMISTIC (blocking calls only)
   unsigned long long zstat_hits = 0, zstat_exchanges = 0;
   std::vector<LocalReg> lreg;

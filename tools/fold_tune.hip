@@ -60,6 +60,31 @@ __global__ __launch_bounds__(256) void copy1(const f32x4* s, f32x4* d, long long
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i < nv) d[i] = __builtin_nontemporal_load(s + i);
 }
+// placement / store-policy experiments on the 8 -> 1 f32 SUM stream (U = 4
+// vectors per thread, the product's pairwise tree):
+//   SP = 0 plain stores, 1 nt stores, 2 sc1 (write-through) stores
+//   SHIFT: the result of vector i is written to out[(i + SHIFT) mod nv] —
+//   same bytes, but the write stream no longer shares the reads' offsets
+template <int SP, long long SHIFT>
+__global__ __launch_bounds__(256) void exp4(P8 a) {
+  const long long base = (long long)blockIdx.x * 1024 + threadIdx.x;
+  f32x4 v[4][8];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[u][k] = __builtin_nontemporal_load(a.in[k] + base + u * 256);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const f32x4 r = ((v[u][0] + v[u][1]) + (v[u][2] + v[u][3])) + ((v[u][4] + v[u][5]) + (v[u][6] + v[u][7]));
+    long long j = base + u * 256 + SHIFT;
+    if (j >= a.nv) j -= a.nv;
+    f32x4* q = a.out + j;
+    if constexpr (SP == 0) *q = r;
+    else if constexpr (SP == 1) __builtin_nontemporal_store(r, q);
+    else asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(q), "v"(r) : "memory");
+  }
+}
+
 // exhaustive f32 -> bf16: hardware pair conversion vs the software RNE; each
 // thread checks 16 pairs, one atomic per block (bounded even if all differ)
 __global__ __launch_bounds__(256) void cvt_check(unsigned long long base, unsigned long long* bad, unsigned* first) {
@@ -112,6 +137,8 @@ FoldArgs make_args(void* const* in, void* out, long long count, int es) {
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 7;
   const long long S = 256ll << 20;  // bytes per buffer
+  void* outb;
+  CK(hipMalloc(&outb, S));  // allocated before the inputs
   void* in[8];
   for (int k = 0; k < 8; ++k) {
     CK(hipMalloc(&in[k], S));
@@ -142,43 +169,30 @@ int main(int argc, char** argv) {
     std::function<hipError_t()> go;
   };
   const double B9 = 9.0 * S;
-  // layouts: separate 256 MiB allocations (af/ab), one slab with the inputs
-  // S apart (a0), the slab with a 68 KiB stagger (as), separate allocations
-  // with the pointer offset k * 68 KiB into each (ao)
-  char* slab0;
-  CK(hipMalloc((void**)&slab0, 8 * S));
-  CK(hipMemset(slab0, 0x3c, 8 * S));
-  void *in0[8], *ino[8];
-  for (int k = 0; k < 8; ++k) {
-    in0[k] = slab0 + k * S;
-    void* q;
-    CK(hipMalloc(&q, S + 8 * stag));
-    CK(hipMemset(q, 0x3c, S + 8 * stag));
-    ino[k] = (char*)q + k * stag;
-  }
-  FoldArgs a0 = make_args(in0, out, cf, 4), ao = make_args(ino, out, cf, 4);
-  FoldArgs asb = make_args(sin, out, cb, 2);
+  // output placements: out allocated after the inputs (out2 / out), an
+  // output allocated BEFORE them (outb), an output 68 KiB into its allocation
+  char* outo_raw;
+  CK(hipMalloc((void**)&outo_raw, S + stag));
+  void* outo = outo_raw + stag;
+  FoldArgs ab4 = make_args(in, outb, cf, 4), ao4 = make_args(in, outo, cf, 4);
+  P8 pb = p, po = p, pa = p;
+  pb.out = (f32x4*)outb;
+  po.out = (f32x4*)outo;
+  pa.out = (f32x4*)out;
+  const unsigned G4 = (unsigned)(p.nv / 1024);
   std::vector<V> vs = {
-      {"f32 SUM U1 pow2 (r01 shape)", B9, [&] { return launch_prod<OpSum, float, 1, SH_POW2>(af); }},
-      {"f32 SUM U1", B9, [&] { return launch_prod<OpSum, float, 1>(af); }},
-      {"f32 SUM U2", B9, [&] { return launch_prod<OpSum, float, 2>(af); }},
-      {"f32 SUM U4", B9, [&] { return launch_prod<OpSum, float, 4>(af); }},
-      {"f32 SUM U1 slab0", B9, [&] { return launch_prod<OpSum, float, 1>(a0); }},
-      {"f32 SUM U4 slab0", B9, [&] { return launch_prod<OpSum, float, 4>(a0); }},
-      {"f32 SUM U1 stag", B9, [&] { return launch_prod<OpSum, float, 1>(as); }},
-      {"f32 SUM U4 stag", B9, [&] { return launch_prod<OpSum, float, 4>(as); }},
-      {"f32 SUM U1 ptroff", B9, [&] { return launch_prod<OpSum, float, 1>(ao); }},
-      {"f32 SUM U4 ptroff", B9, [&] { return launch_prod<OpSum, float, 4>(ao); }},
-      {"f32 MAX U1", B9, [&] { return launch_prod<OpMax, float, 1>(af); }},
-      {"f32 MAX U2", B9, [&] { return launch_prod<OpMax, float, 2>(af); }},
-      {"f32 MAX U4", B9, [&] { return launch_prod<OpMax, float, 4>(af); }},
-      {"bf16 SUM U2", B9, [&] { return launch_prod<OpSum, bf16, 2>(ab); }},
-      {"bf16 SUM U4", B9, [&] { return launch_prod<OpSum, bf16, 4>(ab); }},
-      {"bf16 MAX U1", B9, [&] { return launch_prod<OpMax, bf16, 1>(ab); }},
-      {"bf16 MAX U2", B9, [&] { return launch_prod<OpMax, bf16, 2>(ab); }},
-      {"bf16 SUM U4 stag", B9, [&] { return launch_prod<OpSum, bf16, 4>(asb); }},
-      {"bf16 MAX U2 stag", B9, [&] { return launch_prod<OpMax, bf16, 2>(asb); }},
-      {"ref once plainS", B9, [&] { hipLaunchKernelGGL((ref_once<false, false>), dim3(G1), dim3(256), 0, 0, p); return hipGetLastError(); }},
+      {"prod f32 SUM U4 out-after", B9, [&] { return launch_prod<OpSum, float, 4>(af); }},
+      {"prod f32 SUM U4 out-before", B9, [&] { return launch_prod<OpSum, float, 4>(ab4); }},
+      {"prod f32 SUM U4 out+68K", B9, [&] { return launch_prod<OpSum, float, 4>(ao4); }},
+      {"prod f32 SUM U4 stag inputs", B9, [&] { return launch_prod<OpSum, float, 4>(as); }},
+      {"exp plain shift0", B9, [&] { hipLaunchKernelGGL((exp4<0, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp nt shift0", B9, [&] { hipLaunchKernelGGL((exp4<1, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp sc1 shift0", B9, [&] { hipLaunchKernelGGL((exp4<2, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp plain shift16M", B9, [&] { hipLaunchKernelGGL((exp4<0, (1 << 20)>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp plain shift68K", B9, [&] { hipLaunchKernelGGL((exp4<0, 4352>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp sc1 shift16M", B9, [&] { hipLaunchKernelGGL((exp4<2, (1 << 20)>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp plain shift0 out-before", B9, [&] { hipLaunchKernelGGL((exp4<0, 0>), dim3(G4), dim3(256), 0, 0, pb); return hipGetLastError(); }},
+      {"exp plain shift0 out+68K", B9, [&] { hipLaunchKernelGGL((exp4<0, 0>), dim3(G4), dim3(256), 0, 0, po); return hipGetLastError(); }},
       {"read 8 streams", 8.0 * S, [&] { hipLaunchKernelGGL(read8, dim3(G1), dim3(256), 0, 0, p); return hipGetLastError(); }},
       {"copy 256MiB", 2.0 * S, [&] { hipLaunchKernelGGL(copy1, dim3(G1), dim3(256), 0, 0, (const f32x4*)in[0], (f32x4*)out2, p.nv); return hipGetLastError(); }},
   };

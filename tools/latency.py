@@ -49,11 +49,15 @@ for nbytes in SIZES:
         h0, x0 = stats()
         it = 200 if nbytes <= (8 << 20) else 30
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(it)]
+        pre = []
         t0 = time.perf_counter()
         for a, b in ev:
             a.record(s)
             call()
             b.record(s)
+            p_ = ctypes.c_double()
+            L.mpigx_comm_host_stats(comm.val, ctypes.byref(p_))
+            pre.append(p_.value)
         L.mpigx_comm_synchronize(comm.val)
         dt = (time.perf_counter() - t0) / it
         torch.cuda.synchronize()
@@ -61,7 +65,9 @@ for nbytes in SIZES:
         h1, x1 = stats()
         L.mpigx_comm_set_blocking(comm.val, 1)
         key = f"{nbytes}B_{mode}"
-        res[key] = {"wall_us": round(dt * 1e6, 2), "device_us": round(dev * 1e6, 2)}
+        pre.sort()
+        res[key] = {"wall_us": round(dt * 1e6, 2), "device_us": round(dev * 1e6, 2),
+                    "prelaunch_us_median": round(pre[len(pre) // 2], 2)}
         if mode != "raw_nonblocking":
             res[key]["host_us"] = round((dt - dev) * 1e6, 2)
         if nbytes >= (16 << 20):

@@ -59,7 +59,7 @@ def main(out, dest, tag):
     # the headline kernel, keyed for bench.py
     j = {"kernels": summary}
     for k in summary:
-        if "fold_local_kernel<mpigx::OpSum, float, 8, 0>" in k or "fold_local_kernelINS_5OpSumEfLi8ELi0E" in k:
+        if "fold_local_kernel<mpigx::OpSum, float, 8, 0" in k or "fold_local_kernelINS_5OpSumEfLi8ELi0E" in k:
             j["reduce_local_multi_f32_sum_8x256MiB"] = summary[k]["hbm_bytes_per_dispatch"]
     with open(os.path.join(dest, f"{tag}_traffic.json"), "w") as fh:
         json.dump(j, fh, indent=1)
