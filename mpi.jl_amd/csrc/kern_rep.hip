@@ -1,5 +1,12 @@
-// kern_rep.hip — instantiates the fold and scan kernels for ONE element
-// representation (compiled once per Rep; see Makefile) and exposes launchers.
+// kern_rep.hip — instantiates the fold / ring / scan / accumulate kernels of
+// ONE element representation and exposes launchers.  Compiled once per
+// (Rep, part) (see Makefile):
+//   -DMPIGX_REP=<Rep> -DMPIGX_REP_NAME=<name> -DMPIGX_PART=<0..6>
+// Parts 0-5 each instantiate the kernels of a few ops (the role-sensitive
+// MIN / MAX trees of the packed bf16 type alone take minutes to compile, so
+// one translation unit per rep serialised the build); part 6 holds MPI_REPLACE
+// / MPI_NO_OP (accumulate only) and the per-rep dispatchers launch.hpp
+// declares, which call the other parts through per-op entry points.
 // Only the (op, type) pairs MPICH accepts are instantiated (op x type matrix:
 // tests/golden/op_type_matrix.json); the host rejects the rest with
 // MPI_ERR_OP before launching.
@@ -7,16 +14,46 @@
 #include "launch.hpp"
 
 #ifndef MPIGX_REP
-#error "compile with -DMPIGX_REP=<Rep> -DMPIGX_REP_NAME=<name>"
+#error "compile with -DMPIGX_REP=<Rep> -DMPIGX_REP_NAME=<name> -DMPIGX_PART=<part>"
+#endif
+#ifndef MPIGX_PART
+#error "compile with -DMPIGX_PART=<0..6>"
 #endif
 #define MPIGX_CAT2(a, b) a##b
 #define MPIGX_CAT(a, b) MPIGX_CAT2(a, b)
+#define MPIGX_CAT4(a, b, c, d) MPIGX_CAT(MPIGX_CAT(a, b), MPIGX_CAT(c, d))
+
+// per-op entry points of this rep: launch_<kind>_<name>_o<op code>
+#define MPIGX_FOLD_FN(K) MPIGX_CAT4(launch_fold_, MPIGX_REP_NAME, _o, K)
+#define MPIGX_RING_FN(K) MPIGX_CAT4(launch_ring_, MPIGX_REP_NAME, _o, K)
+#define MPIGX_SCAN_FN(K) MPIGX_CAT4(launch_scan_, MPIGX_REP_NAME, _o, K)
+#define MPIGX_ACC_FN(K) MPIGX_CAT4(launch_acc_, MPIGX_REP_NAME, _o, K)
 
 namespace mpigx {
 namespace {
 using T = RepType<MPIGX_REP>::T;
 constexpr bool kInt = is_int<T>::v;
 constexpr bool kCplx = is_cplx<T>::v;
+
+// the op x type matrix (collectives); accumulate adds REPLACE / NO_OP
+constexpr bool valid_op(int op) {
+  return op == O_SUM || op == O_PROD || (!kCplx && op >= O_MIN && op <= O_LXOR) ||
+         (kInt && op >= O_BAND && op <= O_BXOR);
+}
+
+template <int K> struct OpOf;
+template <> struct OpOf<O_SUM> { using type = OpSum; };
+template <> struct OpOf<O_PROD> { using type = OpProd; };
+template <> struct OpOf<O_MIN> { using type = OpMin; };
+template <> struct OpOf<O_MAX> { using type = OpMax; };
+template <> struct OpOf<O_LAND> { using type = OpLand; };
+template <> struct OpOf<O_LOR> { using type = OpLor; };
+template <> struct OpOf<O_LXOR> { using type = OpLxor; };
+template <> struct OpOf<O_BAND> { using type = OpBand; };
+template <> struct OpOf<O_BOR> { using type = OpBor; };
+template <> struct OpOf<O_BXOR> { using type = OpBxor; };
+template <> struct OpOf<O_REPLACE> { using type = OpReplace; };
+template <> struct OpOf<O_NOOP> { using type = OpNoop; };
 
 template <class OP>
 hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a) {
@@ -56,133 +93,118 @@ hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs
   }
   return hipGetLastError();
 }
-template <class OP>
-hipError_t ring_op(dim3 grid, hipStream_t s, const RingArgs& a) {
-  hipLaunchKernelGGL((ring_kernel<OP, T>), grid, dim3(kThreads), 0, s, a);
-  return hipGetLastError();
-}
-template <class OP>
-hipError_t scan_op(dim3 grid, hipStream_t s, const ScanArgs& a) {
-  hipLaunchKernelGGL((scan_kernel<OP, T>), grid, dim3(kThreads), 0, s, a);
-  return hipGetLastError();
-}
-template <class OP>
-hipError_t acc_op(dim3 grid, hipStream_t s, const AccArgs& a) {
-  hipLaunchKernelGGL((acc_kernel<OP, T>), grid, dim3(kThreads), 0, s, a);
-  return hipGetLastError();
-}
 }  // namespace
+
+// Per-op entry points: declared for every op code here (the dispatchers of
+// part 6 reference only the valid ones), defined by the part that owns the op.
+#define MPIGX_DECL_OP(K)                                                                               \
+  hipError_t MPIGX_FOLD_FN(K)(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a);      \
+  hipError_t MPIGX_RING_FN(K)(dim3 grid, hipStream_t s, const RingArgs& a);                            \
+  hipError_t MPIGX_SCAN_FN(K)(dim3 grid, hipStream_t s, const ScanArgs& a);                            \
+  hipError_t MPIGX_ACC_FN(K)(dim3 grid, hipStream_t s, const AccArgs& a);
+MPIGX_DECL_OP(0) MPIGX_DECL_OP(1) MPIGX_DECL_OP(2) MPIGX_DECL_OP(3) MPIGX_DECL_OP(4) MPIGX_DECL_OP(5)
+MPIGX_DECL_OP(6) MPIGX_DECL_OP(7) MPIGX_DECL_OP(8) MPIGX_DECL_OP(9) MPIGX_DECL_OP(16) MPIGX_DECL_OP(17)
+#undef MPIGX_DECL_OP
+
+// Definitions for op code K (a collective op: all four kernel families).
+#define MPIGX_DEF_OP(K)                                                                                \
+  hipError_t MPIGX_FOLD_FN(K)(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a) {     \
+    if constexpr (valid_op(K)) return fold_op<OpOf<K>::type>(nmax, sched, grid, s, a);                 \
+    return hipErrorInvalidValue;                                                                       \
+  }                                                                                                    \
+  hipError_t MPIGX_RING_FN(K)(dim3 grid, hipStream_t s, const RingArgs& a) {                           \
+    if constexpr (valid_op(K)) {                                                                       \
+      hipLaunchKernelGGL((ring_kernel<OpOf<K>::type, T>), grid, dim3(kThreads), 0, s, a);              \
+      return hipGetLastError();                                                                        \
+    }                                                                                                  \
+    return hipErrorInvalidValue;                                                                       \
+  }                                                                                                    \
+  hipError_t MPIGX_SCAN_FN(K)(dim3 grid, hipStream_t s, const ScanArgs& a) {                           \
+    if constexpr (valid_op(K)) {                                                                       \
+      hipLaunchKernelGGL((scan_kernel<OpOf<K>::type, T>), grid, dim3(kThreads), 0, s, a);              \
+      return hipGetLastError();                                                                        \
+    }                                                                                                  \
+    return hipErrorInvalidValue;                                                                       \
+  }                                                                                                    \
+  hipError_t MPIGX_ACC_FN(K)(dim3 grid, hipStream_t s, const AccArgs& a) {                             \
+    if constexpr (valid_op(K)) {                                                                       \
+      hipLaunchKernelGGL((acc_kernel<OpOf<K>::type, T>), grid, dim3(kThreads), 0, s, a);               \
+      return hipGetLastError();                                                                        \
+    }                                                                                                  \
+    return hipErrorInvalidValue;                                                                       \
+  }
+
+#if MPIGX_PART == 0
+MPIGX_DEF_OP(0)
+#elif MPIGX_PART == 1
+MPIGX_DEF_OP(1)
+#elif MPIGX_PART == 2
+MPIGX_DEF_OP(2)
+#elif MPIGX_PART == 3
+MPIGX_DEF_OP(3)
+#elif MPIGX_PART == 4
+MPIGX_DEF_OP(4) MPIGX_DEF_OP(5) MPIGX_DEF_OP(6)
+#elif MPIGX_PART == 5
+MPIGX_DEF_OP(7) MPIGX_DEF_OP(8) MPIGX_DEF_OP(9)
+#elif MPIGX_PART == 6
+// RMA-only ops: accumulate kernels, any type
+hipError_t MPIGX_ACC_FN(16)(dim3 grid, hipStream_t s, const AccArgs& a) {
+  hipLaunchKernelGGL((acc_kernel<OpReplace, T>), grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t MPIGX_ACC_FN(17)(dim3 grid, hipStream_t s, const AccArgs& a) {
+  hipLaunchKernelGGL((acc_kernel<OpNoop, T>), grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+// The per-rep dispatchers (launch.hpp).  Each valid op goes to its part's
+// entry point; invalid pairs never get here (host validation) and would
+// return hipErrorInvalidValue.
+#define MPIGX_SWITCH(FN, ...)                                        \
+  switch (op) {                                                      \
+    case O_SUM: return FN(0)(__VA_ARGS__);                           \
+    case O_PROD: return FN(1)(__VA_ARGS__);                          \
+    default: break;                                                  \
+  }                                                                  \
+  if constexpr (!kCplx) {                                            \
+    switch (op) {                                                    \
+      case O_MIN: return FN(2)(__VA_ARGS__);                         \
+      case O_MAX: return FN(3)(__VA_ARGS__);                         \
+      case O_LAND: return FN(4)(__VA_ARGS__);                        \
+      case O_LOR: return FN(5)(__VA_ARGS__);                         \
+      case O_LXOR: return FN(6)(__VA_ARGS__);                        \
+      default: break;                                                \
+    }                                                                \
+  }                                                                  \
+  if constexpr (kInt) {                                              \
+    switch (op) {                                                    \
+      case O_BAND: return FN(7)(__VA_ARGS__);                        \
+      case O_BOR: return FN(8)(__VA_ARGS__);                         \
+      case O_BXOR: return FN(9)(__VA_ARGS__);                        \
+      default: break;                                                \
+    }                                                                \
+  }                                                                  \
+  return hipErrorInvalidValue;
 
 hipError_t MPIGX_CAT(launch_fold_, MPIGX_REP_NAME)(int op, int nmax, int sched, dim3 grid, hipStream_t s,
                                                   const FoldArgs& a) {
-  switch (op) {
-    case O_SUM: return fold_op<OpSum>(nmax, sched, grid, s, a);
-    case O_PROD: return fold_op<OpProd>(nmax, sched, grid, s, a);
-    default: break;
-  }
-  if constexpr (!kCplx) {
-    switch (op) {
-      case O_MIN: return fold_op<OpMin>(nmax, sched, grid, s, a);
-      case O_MAX: return fold_op<OpMax>(nmax, sched, grid, s, a);
-      case O_LAND: return fold_op<OpLand>(nmax, sched, grid, s, a);
-      case O_LOR: return fold_op<OpLor>(nmax, sched, grid, s, a);
-      case O_LXOR: return fold_op<OpLxor>(nmax, sched, grid, s, a);
-      default: break;
-    }
-  }
-  if constexpr (kInt) {
-    switch (op) {
-      case O_BAND: return fold_op<OpBand>(nmax, sched, grid, s, a);
-      case O_BOR: return fold_op<OpBor>(nmax, sched, grid, s, a);
-      case O_BXOR: return fold_op<OpBxor>(nmax, sched, grid, s, a);
-      default: break;
-    }
-  }
-  return hipErrorInvalidValue;
+  MPIGX_SWITCH(MPIGX_FOLD_FN, nmax, sched, grid, s, a)
 }
-
 hipError_t MPIGX_CAT(launch_ring_, MPIGX_REP_NAME)(int op, dim3 grid, hipStream_t s, const RingArgs& a) {
-  switch (op) {
-    case O_SUM: return ring_op<OpSum>(grid, s, a);
-    case O_PROD: return ring_op<OpProd>(grid, s, a);
-    default: break;
-  }
-  if constexpr (!kCplx) {
-    switch (op) {
-      case O_MIN: return ring_op<OpMin>(grid, s, a);
-      case O_MAX: return ring_op<OpMax>(grid, s, a);
-      case O_LAND: return ring_op<OpLand>(grid, s, a);
-      case O_LOR: return ring_op<OpLor>(grid, s, a);
-      case O_LXOR: return ring_op<OpLxor>(grid, s, a);
-      default: break;
-    }
-  }
-  if constexpr (kInt) {
-    switch (op) {
-      case O_BAND: return ring_op<OpBand>(grid, s, a);
-      case O_BOR: return ring_op<OpBor>(grid, s, a);
-      case O_BXOR: return ring_op<OpBxor>(grid, s, a);
-      default: break;
-    }
-  }
-  return hipErrorInvalidValue;
+  MPIGX_SWITCH(MPIGX_RING_FN, grid, s, a)
 }
-
 hipError_t MPIGX_CAT(launch_scan_, MPIGX_REP_NAME)(int op, dim3 grid, hipStream_t s, const ScanArgs& a) {
-  switch (op) {
-    case O_SUM: return scan_op<OpSum>(grid, s, a);
-    case O_PROD: return scan_op<OpProd>(grid, s, a);
-    default: break;
-  }
-  if constexpr (!kCplx) {
-    switch (op) {
-      case O_MIN: return scan_op<OpMin>(grid, s, a);
-      case O_MAX: return scan_op<OpMax>(grid, s, a);
-      case O_LAND: return scan_op<OpLand>(grid, s, a);
-      case O_LOR: return scan_op<OpLor>(grid, s, a);
-      case O_LXOR: return scan_op<OpLxor>(grid, s, a);
-      default: break;
-    }
-  }
-  if constexpr (kInt) {
-    switch (op) {
-      case O_BAND: return scan_op<OpBand>(grid, s, a);
-      case O_BOR: return scan_op<OpBor>(grid, s, a);
-      case O_BXOR: return scan_op<OpBxor>(grid, s, a);
-      default: break;
-    }
-  }
-  return hipErrorInvalidValue;
+  MPIGX_SWITCH(MPIGX_SCAN_FN, grid, s, a)
 }
-
 // RMA accumulate: the collective op set plus REPLACE / NO_OP (any type).
 hipError_t MPIGX_CAT(launch_acc_, MPIGX_REP_NAME)(int op, dim3 grid, hipStream_t s, const AccArgs& a) {
-  switch (op) {
-    case O_REPLACE: return acc_op<OpReplace>(grid, s, a);
-    case O_NOOP: return acc_op<OpNoop>(grid, s, a);
-    case O_SUM: return acc_op<OpSum>(grid, s, a);
-    case O_PROD: return acc_op<OpProd>(grid, s, a);
-    default: break;
-  }
-  if constexpr (!kCplx) {
-    switch (op) {
-      case O_MIN: return acc_op<OpMin>(grid, s, a);
-      case O_MAX: return acc_op<OpMax>(grid, s, a);
-      case O_LAND: return acc_op<OpLand>(grid, s, a);
-      case O_LOR: return acc_op<OpLor>(grid, s, a);
-      case O_LXOR: return acc_op<OpLxor>(grid, s, a);
-      default: break;
-    }
-  }
-  if constexpr (kInt) {
-    switch (op) {
-      case O_BAND: return acc_op<OpBand>(grid, s, a);
-      case O_BOR: return acc_op<OpBor>(grid, s, a);
-      case O_BXOR: return acc_op<OpBxor>(grid, s, a);
-      default: break;
-    }
-  }
-  return hipErrorInvalidValue;
+  if (op == O_REPLACE) return MPIGX_ACC_FN(16)(grid, s, a);
+  if (op == O_NOOP) return MPIGX_ACC_FN(17)(grid, s, a);
+  MPIGX_SWITCH(MPIGX_ACC_FN, grid, s, a)
 }
+#undef MPIGX_SWITCH
+#else
+#error "MPIGX_PART must be 0..6"
+#endif
 
 }  // namespace mpigx
