@@ -1999,6 +1999,77 @@ static Registry<UserOp, HS_OP> g_userops;
 
 static UserOp* user_op(int h) { return g_userops.get(h); }
 
+// Fold the n contributions x_0..x_{n-1} of `len` elements each, stored in
+// slots `slot` bytes apart at `all` (device), into slot n-1:
+// inout = x_q o inout for q = n-2 .. 0 (the rank order user_reduce uses).
+static int user_fold_slots(mpigx_comm* c, UserOp* u, char* all, long long slot, int n, int len, int dt) {
+  if (len == 0 || n < 2) return MPIGX_SUCCESS;
+  char* inout = all + (long long)(n - 1) * slot;
+  if (u->dev_fn) {
+    for (int q = n - 2; q >= 0; --q) u->dev_fn(all + q * slot, inout, (long long)len, dt, (void*)c->stream);
+    return hipGetLastError() == hipSuccess ? MPIGX_SUCCESS : MPIGX_ERR_OTHER;
+  }
+  char* h = nullptr;
+  if (hipHostMalloc((void**)&h, (size_t)n * slot, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return MPIGX_ERR_NO_MEM;
+  }
+  int rc = MPIGX_SUCCESS;
+  if (hipMemcpyAsync(h, all, (size_t)n * slot, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    rc = MPIGX_ERR_INTERN;
+  for (int q = n - 2; !rc && q >= 0; --q) u->host_fn(h + q * slot, h + (n - 1) * slot, &len, &dt);
+  if (!rc && (hipMemcpyAsync(inout, h + (n - 1) * slot, (size_t)slot, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+              hipStreamSynchronize(c->stream) != hipSuccess))
+    rc = MPIGX_ERR_INTERN;
+  if (rc) (void)hipGetLastError();
+  (void)hipHostFree(h);
+  return rc;
+}
+
+// Allreduce (kind 0) / Reduce (kind 1) with a user op: reduce-scatter +
+// allgather / gather, so each rank receives (n-1)/n of the message, runs n-1
+// callbacks on ITS chunk only and sends its chunk back out — O(S) bytes and
+// O(S) callback work per rank instead of gathering all n contributions
+// (n·S) and folding all of them everywhere.  Chunk k = datatype elements
+// [k·ce, (k+1)·ce), ce = ceil(count/n); every element still sees
+// inout = x_q o inout for q = n-2 .. 0, so results are bit-identical to the
+// all-gather fold (and MPI's canonical order for non-commutative ops).
+static int user_reduce_rs(mpigx_comm* c, UserOp* u, const void* mine, void* recv, int count, int datatype,
+                          long long esz, int root, int kind) {
+  const int n = c->n, r = c->rank;
+  const long long ce = (count + (long long)n - 1) / n;
+  int cnt[kMaxRanks], dsp[kMaxRanks], rcnt[kMaxRanks], rdsp[kMaxRanks];
+  for (int k = 0; k < n; ++k) {
+    const long long lo = std::min((long long)k * ce, (long long)count), hi = std::min(lo + ce, (long long)count);
+    cnt[k] = (int)((hi - lo) * esz);
+    dsp[k] = (int)(lo * esz);
+  }
+  const long long slot = cnt[r];
+  for (int q = 0; q < n; ++q) {
+    rcnt[q] = (int)slot;
+    rdsp[q] = (int)(q * slot);
+  }
+  char* all = tmp_get(c, std::max(16ll, (long long)n * slot));
+  if (!all) return MPIGX_ERR_NO_MEM;
+  // reduce-scatter: chunk r of every rank's contribution -> slot q of `all`
+  int rc = mpigx_alltoallv(mine, cnt, dsp, MPIGX_BYTE, all, rcnt, rdsp, MPIGX_BYTE, c);
+  if (!rc) rc = user_fold_slots(c, u, all, slot, n, (int)(slot / esz), datatype);
+  char* res = all + (long long)(n - 1) * slot;
+  if (!rc && kind == 0) {
+    if (slot && hipMemcpyAsync((char*)recv + dsp[r], res, (size_t)slot, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) {
+      (void)hipGetLastError();
+      rc = MPIGX_ERR_INTERN;
+    }
+    // (stream order: the allgather's flagged launch completes after the copy)
+    if (!rc) rc = mpigx_allgatherv(MPIGX_IN_PLACE, 0, MPIGX_BYTE, recv, cnt, dsp, MPIGX_BYTE, c);
+  } else if (!rc) {
+    rc = mpigx_gatherv(res, (int)slot, MPIGX_BYTE, recv, cnt, dsp, MPIGX_BYTE, root, c);
+  }
+  tmp_put(c, all, 0);
+  return rc;
+}
+
 // kind: 0 allreduce, 1 reduce, 2 scan, 3 exscan
 static int user_reduce(mpigx_comm* c, UserOp* u, const void* send, void* recv, int count, int datatype, int root, int kind) {
   rt::TypeDesc d;
@@ -2011,6 +2082,7 @@ static int user_reduce(mpigx_comm* c, UserOp* u, const void* send, void* recv, i
   if (eb > 0x7fffffff) return MPIGX_ERR_COUNT;
   const void* mine = send == MPIGX_IN_PLACE ? recv : send;
   if (!mine || (!recv && (kind != 1 || r == root))) return MPIGX_ERR_BUFFER;
+  if (kind <= 1 && n > 1) return user_reduce_rs(c, u, mine, recv, count, datatype, d.size, root, kind);
   // every contribution needed here: all (allreduce), at the root (reduce), ranks <= r (scans)
   char* all = tmp_get(c, (long long)n * eb);
   if (!all) return MPIGX_ERR_NO_MEM;

@@ -121,6 +121,39 @@ def cases():
     z = dev(np.arange(4, dtype=np.int64) + rank)
     MPI.Allreduce_(z, opr, comm)
     REC.append({"case": "allreduce_inplace_ref", "z": H(z).tolist()})
+    large_cases(opc, pair)
+
+
+def compose_np(x, y):
+    xv, yv = x.reshape(-1, 2), y.reshape(-1, 2)
+    return np.stack([xv[:, 0] * yv[:, 0], xv[:, 0] * yv[:, 1] + xv[:, 1]], axis=1).reshape(-1)
+
+
+def large_cases(opc, pair):
+    """Reduce-scatter + allgather / gather path on ragged chunks (m pairs not
+    a multiple of n): the non-commutative composition must equal the rank-order
+    fold x0 o (x1 o (... o x_{n-1})) computed on the host; checked here (not
+    recorded: MPICH's fixtures hold the small cases only)."""
+    m = 50021
+    def gen(q):
+        g = np.random.default_rng(500 + q)
+        return np.stack([g.choice([1, 2, -1, 3], m), g.integers(-9, 10, m)], axis=1).astype(np.int64).reshape(-1)
+    xs = [gen(q) for q in range(n)]
+    want = xs[n - 1]
+    for q in range(n - 2, -1, -1):
+        want = compose_np(xs[q], want)
+    x = dev(xs[rank])
+    y = dev(np.zeros(2 * m, np.int64))
+    MPI.Allreduce_(MPI.Buffer(x, m, pair), MPI.Buffer(y, m, pair), opc, comm)
+    assert np.array_equal(H(y), want), "large allreduce_compose"
+    root = n - 1
+    y = dev(np.zeros(2 * m, np.int64))
+    MPI.Reduce_(MPI.Buffer(x, m, pair), MPI.Buffer(y, m, pair), opc, root, comm)
+    if rank == root:
+        assert np.array_equal(H(y), want), "large reduce_compose"
+    z = dev(xs[rank])
+    MPI.Allreduce_(MPI.Buffer(z, m, pair), opc, comm)
+    assert np.array_equal(H(z), want), "large allreduce_compose in place"
 
 
 failed = None
