@@ -67,7 +67,17 @@ enum FoldMode : int {
   M_RED_ZC = 7,       // zero-copy Reduce: barrier, RS of my chunk straight from every
                       // rank's sendbuf into my arena (the root: its recvbuf), barrier,
                       // the root gathers every chunk from the arenas, barrier
+  M_AR_LL = 8,        // small Allreduce, no barrier: push my bytes as flag-carrying
+                      // lines into every peer's LL area, poll my own area for every
+                      // peer's lines, unpack them into my arena, fold locally
 };
+
+// LL ("low-latency") lines of M_AR_LL: 16 bytes = two 8-byte halves
+// {4 payload bytes, 4-byte flag}, each stored with ONE 64-bit store, so a
+// receiver that sees the launch's flag in a half has that half's payload —
+// no fence and no separate signal.  A rank's LL area (uncached HBM,
+// IPC-mapped by every peer) is [2 parities][kMaxRanks senders][ll_stride].
+constexpr int kLLLine = 16;
 
 // Copy-kernel modes (Bcast / Allgather / Alltoall / Barrier).
 //   C_BCAST     : every non-root pulls the whole buffer from the root (small)
@@ -127,7 +137,14 @@ struct FoldArgs {
   const void* send;    // collective modes: my send buffer (may be == recv)
   void* recv;          // output
   char* zc_recv[kMaxRanks];  // M_AR_ZC / M_AR_PUSH: every rank's recvbuf (IPC-mapped; mine = recv)
-  long long slot_bytes;      // M_AR_PUSH: arena bytes per source slot (chunk bytes, 16-B multiple)
+  long long slot_bytes;      // M_AR_PUSH: arena bytes per source slot (chunk bytes, 16-B multiple);
+                             // M_AR_LL: arena bytes per unpacked contribution
+  // M_AR_LL: zc_recv[p] = rank p's LL area (this launch's parity) at my sender
+  // slot; ll_in = my own area (same parity), sender q's lines at q * ll_stride
+  const char* ll_in;
+  long long ll_stride;
+  unsigned ll_flag;    // this launch's flag (never 0, never a stale flag of the same parity)
+  int ll_pad;
 };
 
 // Ring reduce-scatter + allgather (MPIGX_ALGO=ring; kernels.hpp ring_kernel).

@@ -696,4 +696,74 @@ __device__ __forceinline__ bool zc_enter(const PeerView& pv, uint64_t ep, int* a
   return rank_barrier(pv, ep, abort, pv.zc_key, true);
 }
 
+// ---------------------------------------------------------------------------
+// LL exchange (M_AR_LL, common.hpp kLLLine) of lines [l0, l1) of a `bytes`-byte
+// message, the block cooperating.  Line i carries message bytes [8i, 8i+8).
+//   push: my line i -> every peer's area at push[p] + 16 i (two 64-bit
+//         system-scope stores into uncached HBM; over xGMI for other GPUs);
+//         my own bytes -> my unpack slot r
+//   poll: sender q's line i at in + q*stride + 16 i until both halves carry
+//         `flag`, payload -> unpack slot q (my arena, ordinary stores)
+// Every peer's lines land in MY memory, so the only cross-GPU latency is one
+// posted write: no release fence, no signal word, no acquire.  Area reuse:
+// the launch alternates parities; a sender can only reach the next launch of
+// the same parity after it received my lines of the launch in between, which
+// I push only after this launch has finished reading (stream order).
+// Returns false (and sets *pv.err) if a sender does not arrive in time.
+// ---------------------------------------------------------------------------
+__device__ __noinline__ bool ll_exchange(char* const* push, const char* in, long long stride, unsigned flag,
+                                         const char* send, long long bytes, long long l0, long long l1, char* unp,
+                                         long long ustride, int n, int r, uint64_t timeout, unsigned* err) {
+  __shared__ int s_ok;
+  const long long tid = threadIdx.x, nt = blockDim.x;
+  const bool al8 = (((uintptr_t)send) & 7) == 0;
+  const uint64_t fw = (uint64_t)flag << 32;
+  if (tid == 0) s_ok = 1;
+  for (long long i = l0 + tid; i < l1; i += nt) {
+    const long long o = 8 * i;
+    uint64_t d = 0;
+    if (al8 && o + 8 <= bytes) {
+      d = *reinterpret_cast<const uint64_t*>(send + o);
+    } else {
+      for (int k = 0; k < 8; ++k)
+        if (o + k < bytes) d |= (uint64_t)(uint8_t)send[o + k] << (8 * k);
+    }
+    const uint64_t h0 = (d & 0xffffffffull) | fw, h1 = (d >> 32) | fw;
+    for (int p = 0; p < n; ++p) {
+      if (p == r) continue;
+      uint64_t* q = reinterpret_cast<uint64_t*>(push[p] + kLLLine * i);
+      __hip_atomic_store(q, h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(q + 1, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    *reinterpret_cast<uint64_t*>(unp + r * ustride + o) = d;
+  }
+  bool ok = true;
+  const uint64_t t0 = wall_clock64();
+  for (long long i = l0 + tid; i < l1 && ok; i += nt) {
+    for (int p = 0; p < n && ok; ++p) {
+      if (p == r) continue;
+      const uint64_t* q = reinterpret_cast<const uint64_t*>(in + p * stride + kLLLine * i);
+      uint64_t a, b;
+      for (;;) {
+        a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((unsigned)(a >> 32) == flag && (unsigned)(b >> 32) == flag) break;
+        if (wall_clock64() - t0 > timeout) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (ok) *reinterpret_cast<uint64_t*>(unp + p * ustride + 8 * i) = (a & 0xffffffffull) | (b << 32);
+    }
+  }
+  __syncthreads();
+  if (!ok) {
+    s_ok = 0;
+    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();  // the unpacked bytes are visible to the whole block
+  return s_ok != 0;
+}
+
 }  // namespace mpigx

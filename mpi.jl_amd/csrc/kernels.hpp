@@ -303,6 +303,21 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     return ab;
   }
 
+  if (A.mode == M_AR_LL) {
+    // small Allreduce in one step: every rank's slice b arrives as LL lines
+    // in my own memory (device.hpp ll_exchange), unpacked into my arena slot
+    // of its rank; the fold then reads local HBM only, with the same
+    // schedule and leaf order as the one-shot (src[] = the unpack slots)
+    const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
+    const long long bytes = A.count * es;
+    const long long l0 = (lo * es) / 8, l1 = hi > lo ? (hi * es + 7) / 8 : l0;
+    if (!ll_exchange(A.zc_recv, A.ll_in, A.ll_stride, A.ll_flag, send, bytes, l0, l1, (char*)mine, A.slot_bytes,
+                     pv.n, pv.rank, pv.timeout_ticks, pv.err))
+      return 0;
+    fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
+    return 0;
+  }
+
   if (A.mode == M_AR_ONESHOT || A.mode == M_RED_ONESHOT) {
     const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
     block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);

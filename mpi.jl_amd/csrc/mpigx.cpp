@@ -803,6 +803,37 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     if (rc || !staged) return rc;
     if (c->zc_require) return MPIGX_ERR_INTERN;
   }
+  // small Allreduce: one LL step (no barrier, kernels.hpp M_AR_LL); the
+  // unpacked contributions take n slots of the arena
+  const long long ustride = rup(c->ll_max, 16);
+  if (all && c->ll && count * es <= c->ll_max && (long long)n * ustride <= (long long)c->stage_bytes &&
+      !(algo_env && (!strcmp(algo_env, "oneshot") || !strcmp(algo_env, "twoshot")))) {
+    FoldArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.mode = M_AR_LL;
+    a.esize = es;
+    a.count = count;
+    a.send = send;
+    a.recv = recv;
+    const long long par = (long long)(c->ll_seq & 1) * kMaxRanks * c->ll_stride;
+    for (int p = 0; p < n; ++p) a.zc_recv[p] = c->peer_ll[p] + par + (long long)c->rank * c->ll_stride;
+    a.ll_in = c->ll + par;
+    a.ll_stride = c->ll_stride;
+    a.ll_flag = (unsigned)(c->epoch & 0x7fffffffu) | 0x80000000u;
+    a.slot_bytes = ustride;
+    int nmax, sched;
+    const void* ptrs[kMaxRanks];
+    for (int p = 0; p < n; ++p) ptrs[p] = c->stage + p * ustride;
+    plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
+    const int grid = grid_for(c, count * es);
+    a.slice = rup(cdiv(count, grid), vec);
+    HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
+    note_launch(c, a.pv, grid);
+    c->epoch += 1;
+    c->ll_seq += 1;
+    return finish(c);
+  }
   for (long long off = 0; off < count; off += round) {
     const long long cnt = count - off < round ? count - off : round;
     FoldArgs a;
@@ -1119,6 +1150,7 @@ void comm_release(mpigx_comm* c) {
   for (int q = 0; q < c->n; ++q) {
     if (c->peer_opened[q]) (void)hipIpcCloseMemHandle(c->peer_stage[q]);
     if (c->peer_sig_opened[q]) (void)hipIpcCloseMemHandle(c->peer_sig[q]);
+    if (c->peer_ll_opened[q]) (void)hipIpcCloseMemHandle(c->peer_ll[q]);
   }
   for (auto& im : c->imports) (void)hipIpcCloseMemHandle(im.base);
   if (c->shm) munmap(c->shm, sizeof(ShmBlock));
@@ -1126,6 +1158,7 @@ void comm_release(mpigx_comm* c) {
   for (auto& b : c->tmp_used) (void)hipFree(b.second);
   if (c->stage) (void)hipFree(c->stage);
   if (c->sig) (void)hipFree(c->sig);
+  if (c->ll) (void)hipFree(c->ll);
   if (c->dcount_dev) (void)hipFree(c->dcount_dev);
   if (c->err) (void)hipHostFree(c->err);
   (void)hipGetLastError();
@@ -1156,6 +1189,17 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   const size_t sig_bytes = (size_t)kMaxBlocks * kMaxRanks * sizeof(uint64_t);
   HIPCK(hipExtMallocWithFlags((void**)&c->sig, sig_bytes, hipDeviceMallocUncached));
   HIPCK(hipMemset(c->sig, 0, sig_bytes));
+  // LL area for small Allreduce (M_AR_LL): uncached like the signal array, so
+  // peers' 64-bit line stores and my polls meet in HBM with no cache in between
+  c->ll_max = env_ll("MPIGX_LL_MAX", 64 << 10);
+  if (c->ll_max < 0) c->ll_max = 0;
+  if (c->ll_max > (4ll << 20)) c->ll_max = 4ll << 20;
+  c->ll_stride = rup(c->ll_max, 16) / 8 * kLLLine;
+  if (c->ll_max > 0 && nranks > 1) {
+    const size_t llb = (size_t)2 * kMaxRanks * c->ll_stride;
+    HIPCK(hipExtMallocWithFlags((void**)&c->ll, llb, hipDeviceMallocUncached));
+    HIPCK(hipMemset(c->ll, 0, llb));
+  }
   HIPCK(hipHostMalloc((void**)&c->err, 64, hipHostMallocCoherent | hipHostMallocMapped));
   memset(c->err, 0, 64);
   HIPCK(hipHostGetDevicePointer((void**)&c->err_dev, c->err, 0));
@@ -1168,6 +1212,7 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   HIPCK(hipDeviceSynchronize());
   c->peer_stage[rank] = c->stage;
   c->peer_sig[rank] = c->sig;
+  c->peer_ll[rank] = c->ll;
   if (nranks == 1) return MPIGX_SUCCESS;
 
   // rendezvous
@@ -1222,6 +1267,9 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   me.sig_ptr = (unsigned long long)(uintptr_t)c->sig;
   HIPCK(hipIpcGetMemHandle(&me.stage_h, c->stage));
   HIPCK(hipIpcGetMemHandle(&me.sig_h, c->sig));
+  me.ll_bytes = c->ll ? (unsigned long long)c->ll_max : 0;
+  me.ll_ptr = (unsigned long long)(uintptr_t)c->ll;
+  if (c->ll) HIPCK(hipIpcGetMemHandle(&me.ll_h, c->ll));
   c->shm->arrived.fetch_add(1, std::memory_order_acq_rel);
   while (c->shm->arrived.load(std::memory_order_acquire) < nranks) {
     if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
@@ -1231,10 +1279,12 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
     if (q == rank) continue;
     const ShmRank& pr = c->shm->ranks[q];
     if (pr.stage_bytes != c->stage_bytes) return MPIGX_ERR_ARG;  // MPIGX_STAGING_BYTES must agree
+    if (pr.ll_bytes != me.ll_bytes) return MPIGX_ERR_ARG;        // MPIGX_LL_MAX likewise
     c->same_device[q] = pr.pci_bus == me.pci_bus && pr.pci_dev == me.pci_dev;
     if (pr.pid == me.pid) {
       c->peer_stage[q] = (char*)(uintptr_t)pr.stage_ptr;
       c->peer_sig[q] = (uint64_t*)(uintptr_t)pr.sig_ptr;
+      c->peer_ll[q] = (char*)(uintptr_t)pr.ll_ptr;
     } else {
       void* ps = nullptr;
       void* pg = nullptr;
@@ -1244,6 +1294,12 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
       HIPCK(hipIpcOpenMemHandle(&pg, pr.sig_h, hipIpcMemLazyEnablePeerAccess));
       c->peer_sig[q] = (uint64_t*)pg;
       c->peer_sig_opened[q] = true;
+      if (c->ll) {
+        void* pl = nullptr;
+        HIPCK(hipIpcOpenMemHandle(&pl, pr.ll_h, hipIpcMemLazyEnablePeerAccess));
+        c->peer_ll[q] = (char*)pl;
+        c->peer_ll_opened[q] = true;
+      }
     }
   }
   c->shm->connected.fetch_add(1, std::memory_order_acq_rel);

@@ -27,6 +27,9 @@ struct ShmRank {
   unsigned long long sig_ptr;
   hipIpcMemHandle_t stage_h;
   hipIpcMemHandle_t sig_h;
+  unsigned long long ll_bytes;   // LL area size (0: none; must agree on every rank)
+  unsigned long long ll_ptr;
+  hipIpcMemHandle_t ll_h;
   // host control-plane exchange (host_allgather): double-buffered blobs
   std::atomic<uint64_t> xseq;
   char xbuf[2][256];
@@ -122,6 +125,10 @@ struct mpigx_comm {
   char* stage = nullptr;
   size_t stage_bytes = 0;
   uint64_t* sig = nullptr;
+  char* ll = nullptr;          // LL area (uncached): [2 parities][kMaxRanks senders][ll_stride]
+  long long ll_max = 0;        // MPIGX_LL_MAX: Allreduce bytes that take M_AR_LL (0: off)
+  long long ll_stride = 0;     // bytes of one sender's lines (2 x ll_max rounded to 16)
+  unsigned long long ll_seq = 0;  // LL launches so far (parity = ll_seq & 1; same on every rank)
   unsigned* err = nullptr;  // host-pinned, device-written
   unsigned* err_dev = nullptr;
   // completion counter for blocking calls (host-pinned; kernels add 1 per block)
@@ -184,6 +191,8 @@ struct mpigx_comm {
   uint64_t* peer_sig[mpigx::kMaxRanks] = {};
   bool peer_opened[mpigx::kMaxRanks] = {};      // peer_stage[q] is an IPC mapping of ours
   bool peer_sig_opened[mpigx::kMaxRanks] = {};  // peer_sig[q] likewise
+  char* peer_ll[mpigx::kMaxRanks] = {};         // every rank's LL area (IPC-mapped)
+  bool peer_ll_opened[mpigx::kMaxRanks] = {};
   bool same_device[mpigx::kMaxRanks] = {};      // rank q runs on my GPU (PCI bus/device id)
   mpigx::ShmBlock* shm = nullptr;
   // point-to-point engine (created on first use)

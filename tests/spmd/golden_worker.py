@@ -27,7 +27,9 @@ from oracle import mpich_model as M  # noqa: E402
 IN_PLACE = ctypes.c_void_p(-1 & ((1 << 64) - 1))
 # Allreduce algorithms to run every case through; the push two-shot needs the
 # zero-copy mapping, so it joins when the zero-copy test forces that path
-AR_ALGOS = ("oneshot", "twoshot") + (("push",) if os.environ.get("MPIGX_ZC_MIN") else ())
+# "ll": the default choice (M_AR_LL for Allreduce <= MPIGX_LL_MAX, the
+# staged / zero-copy algorithms above it); "oneshot"/"twoshot" force those
+AR_ALGOS = ("ll", "oneshot", "twoshot") + (("push",) if os.environ.get("MPIGX_ZC_MIN") else ())
 
 
 def dev(a):
@@ -264,6 +266,50 @@ class Runner:
             got = self.run("bcast", ins1, "UINT8_T", None, count, root=1 % n)
             self.check(same_bits(got, ins1[1 % n]), ("bcast-u8", count))
 
+    def ll_cases(self):
+        """M_AR_LL (small Allreduce, default up to MPIGX_LL_MAX = 64 KiB):
+        byte counts around the 8-byte line and the 64 KiB limit, unaligned
+        send buffers, IN_PLACE, and a stream-ordered burst of back-to-back
+        LL launches (both area parities reused while peers run ahead) with
+        other collectives between them; vs the MPICH-pinned oracle."""
+        L, n, r, cv = self.L, self.n, self.r, self.comm.val
+        cases = (("UINT8_T", "BXOR", 1), ("UINT8_T", "SUM", 7), ("INT16_T", "MAX", 5), ("FLOAT", "SUM", 2),
+                 ("FLOAT", "SUM", 3), ("DOUBLE", "PROD", 9), ("C_FLOAT_COMPLEX", "PROD", 17),
+                 ("BFLOAT16", "SUM", 4099), ("INT64_T", "BAND", 1023), ("FLOAT", "MIN", 16384),
+                 ("FLOAT", "SUM", 16385), ("UINT8_T", "BOR", 65536), ("UINT8_T", "BOR", 65537))
+        for i, (dt, op, count) in enumerate(cases):
+            ins = make(dt, op, n, count, 4000 + i, edge=op in ("MAX", "MIN"))
+            exp = M.allreduce(ins, dt, op)[r]
+            for inplace in (False, True):
+                got = self.run("allreduce", ins, dt, op, count, inplace=inplace)
+                self.check(same_bits(got, exp, dt == "BFLOAT16"), ("ll", dt, op, count, inplace))
+        # send buffer at an odd address (byte lines read bytewise)
+        ins = make("UINT8_T", "SUM", n, 1001, 4100)
+        raw = dev(np.concatenate([np.zeros(1, np.uint8), ins[r]]))
+        recv = dev(np.zeros(1001, np.uint8))
+        assert L.mpigx_allreduce(ctypes.c_void_p(raw.data_ptr() + 1), P(recv), 1001, M.DTYPES["UINT8_T"][0],
+                                 M.OPS["SUM"], cv) == 0
+        self.check(same_bits(host(recv, np.uint8), M.allreduce(ins, "UINT8_T", "SUM")[r]), "ll-odd-address")
+        # stream-ordered burst: 40 LL launches (sizes vary, so grids vary) and a
+        # Bcast every 7th, no host wait in between
+        burst, outs = [], []
+        for k in range(40):
+            count = (1, 33, 4096, 16384)[k % 4] + k
+            ins = make("FLOAT", "SUM", n, count, 4200 + k)
+            burst.append((ins, count, dev(ins[r]), dev(np.zeros(count * 4, np.uint8))))
+        bc = dev(np.full(64, r, np.uint8))
+        L.mpigx_comm_set_blocking(cv, 0)
+        for k, (ins, count, s, d) in enumerate(burst):
+            assert L.mpigx_allreduce(P(s), P(d), count, M.DTYPES["FLOAT"][0], M.OPS["SUM"], cv) == 0
+            if k % 7 == 6:
+                assert L.mpigx_bcast(P(bc), 64, M.DTYPES["UINT8_T"][0], k % n, cv) == 0
+        assert L.mpigx_comm_synchronize(cv) == 0
+        L.mpigx_comm_set_blocking(cv, 1)
+        for k, (ins, count, s, d) in enumerate(burst):
+            self.check(same_bits(host(d, np.float32), M.allreduce(ins, "FLOAT", "SUM")[r]), ("ll-burst", k, count))
+        # the first Bcast (k = 6) spreads root 6 % n's value; later ones re-send it
+        self.check(bool((host(bc, np.uint8) == 6 % n).all()), "ll-burst-bcast")
+
     def ring_cases(self, nchs=(1, 2, 4)):
         """MPIGX_ALGO=ring (zero-copy path): bit-exact against the ring's own
         association (oracle fold_ring, rounds included), and against MPICH:
@@ -324,6 +370,7 @@ def main():
         R.golden()
         R.vgolden()
     R.errors()
+    R.ll_cases()
     R.oracle_cases([("FLOAT", "SUM", 1_000_003), ("DOUBLE", "SUM", 65537), ("FLOAT", "MAX", 100_001),
                     ("INT32_T", "BAND", 262_147), ("INT64_T", "MAX", 50_000), ("BFLOAT16", "SUM", 40_000),
                     ("C_FLOAT_COMPLEX", "PROD", 3333), ("UINT8_T", "BXOR", 100_000)])
