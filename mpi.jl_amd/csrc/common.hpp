@@ -70,6 +70,8 @@ enum FoldMode : int {
   M_AR_LL = 8,        // small Allreduce, no barrier: push my bytes as flag-carrying
                       // lines into every peer's LL area, poll my own area for every
                       // peer's lines, unpack them into my arena, fold locally
+  M_RED_LL = 9,       // small Reduce: the same exchange (every rank receives from every
+                      // rank, which keeps the area parities safe), only the root folds
 };
 
 // LL ("low-latency") lines of M_AR_LL: 16 bytes = two 8-byte halves
@@ -90,7 +92,13 @@ enum CopyMode : int {
   C_ALLTOALL_ZC = 7,  // zero-copy: pull block r straight from every rank's (IPC-mapped) sendbuf
   C_ALLGATHER_ZC = 8, // zero-copy: pull block p straight from rank p's sendbuf (or its recvbuf block p)
   C_BCAST_ZC = 9,     // zero-copy: every non-root pulls the root's buffer
-  C_BCAST_SAG_ZC = 10 // zero-copy scatter + allgather between the user buffers
+  C_BCAST_SAG_ZC = 10, // zero-copy scatter + allgather between the user buffers
+  // LL (small messages, no barrier; device.hpp ll_exchange's protocol): every
+  // rank pushes lines into every peer's LL area — its data, or one token line
+  // when it has nothing to send (Bcast non-roots), so every rank receives from
+  // every rank and the area parities stay safe — and unpacks what it needs
+  // straight into the user buffer
+  C_BCAST_LL = 11, C_ALLGATHER_LL = 12, C_ALLTOALL_LL = 13
 };
 
 // Per-call view of the communicator, passed by value to every kernel.
@@ -181,6 +189,11 @@ struct CopyArgs {
   const char* zsrc[kMaxRanks];  // alltoall-zc: every rank's sendbuf (IPC-mapped; mine = send)
   const void* send;
   void* recv;
+  char* ll_push[kMaxRanks];     // LL modes: rank p's LL area (parity) at my sender slot
+  const char* ll_in;            // my own LL area (parity)
+  long long ll_stride;
+  unsigned ll_flag;
+  int ll_pad;
 };
 
 // Personalised exchange (Gather(v) / Scatter(v) / Allgatherv / Alltoallv):
@@ -252,11 +265,18 @@ struct ScanArgs {
   int exclusive;
   int esize;
   int zc;              // 1: operands straight from the peers' sendbufs (src[], zero-copy view)
+  int ll;              // 1: LL exchange (FoldArgs M_AR_LL fields below), src[] = my unpack slots
   long long count;
   long long slice;
   const void* send;
   void* recv;
   const char* src[kMaxRanks];  // rank q's contribution: its staging arena, or its sendbuf (zc)
+  char* ll_push[kMaxRanks];
+  const char* ll_in;
+  long long ll_stride;
+  long long ll_ustride;
+  unsigned ll_flag;
+  int ll_pad;
 };
 
 }  // namespace mpigx

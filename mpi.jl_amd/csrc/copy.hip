@@ -12,8 +12,56 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A);
 
 template <int NMAX>
 __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
-  const int ab = copy_body<NMAX>(A);
-  signal_done(A.pv, ab);
+  // per-rank arrays are indexed at run time: staged in LDS (kernels.hpp)
+  __shared__ CopyArgs sA;
+  static_assert(sizeof(CopyArgs) % 4 == 0, "CopyArgs word copy");
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&A);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
+  for (unsigned i = threadIdx.x; i < sizeof(CopyArgs) / 4; i += blockDim.x) d[i] = w[i];
+  __syncthreads();
+  const int ab = copy_body<NMAX>(sA);
+  signal_done(sA.pv, ab);
+}
+
+// LL lines of byte messages (common.hpp kLLLine; device.hpp ll_exchange):
+// message bytes [8i, 8i+8) of `src` (zero-padded past `bytes`)
+__device__ __forceinline__ uint64_t ll_pack8(const char* src, long long i, long long bytes) {
+  const long long o = 8 * i;
+  if ((((uintptr_t)src) & 7) == 0 && o + 8 <= bytes) return *reinterpret_cast<const uint64_t*>(src + o);
+  uint64_t d = 0;
+  for (int k = 0; k < 8; ++k)
+    if (o + k < bytes) d |= (uint64_t)(uint8_t)src[o + k] << (8 * k);
+  return d;
+}
+__device__ __forceinline__ void ll_put(char* area, long long i, uint64_t d, unsigned flag) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(area + kLLLine * i);
+  const uint64_t fw = (uint64_t)flag << 32;
+  __hip_atomic_store(q, (d & 0xffffffffull) | fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(q + 1, (d >> 32) | fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// waits for line i of a sender's area to carry `flag`; false on timeout
+__device__ __forceinline__ bool ll_get(const char* area, long long i, unsigned flag, uint64_t t0, uint64_t timeout,
+                                       uint64_t* d) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(area + kLLLine * i);
+  for (;;) {
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((unsigned)(a >> 32) == flag && (unsigned)(b >> 32) == flag) {
+      *d = (a & 0xffffffffull) | (b << 32);
+      return true;
+    }
+    if (wall_clock64() - t0 > timeout) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// bytes [8i, 8i+8) ∩ [0, bytes) of dst <- d
+__device__ __forceinline__ void ll_store8(char* dst, long long i, long long bytes, uint64_t d) {
+  const long long o = 8 * i;
+  if ((((uintptr_t)dst) & 7) == 0 && o + 8 <= bytes) {
+    *reinterpret_cast<uint64_t*>(dst + o) = d;
+    return;
+  }
+  for (int k = 0; k < 8 && o + k < bytes; ++k) dst[o + k] = (char)(d >> (8 * k));
 }
 
 // Slice b of chunk k of a chunked byte range: [k*chunk, (k+1)*chunk) ∩ [0,bytes).
@@ -53,6 +101,45 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     }
     if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u) reinterpret_cast<u32x4*>(mine)[threadIdx.x] = acc;
     rank_barrier(pv, ep++);
+    return 0;
+  }
+  if (A.mode == C_BCAST_LL || A.mode == C_ALLGATHER_LL || A.mode == C_ALLTOALL_LL) {
+    // block b: lines of byte slice [lo, hi) of every rank's block; no barrier
+    const long long tid = threadIdx.x, nt = blockDim.x;
+    const unsigned flag = A.ll_flag;
+    const long long l0 = lo / 8, l1 = hi > lo ? (hi + 7) / 8 : l0;
+    const bool bc = A.mode == C_BCAST_LL, a2a = A.mode == C_ALLTOALL_LL;
+    if (!bc || r == A.root) {
+      for (long long i = l0 + tid; i < l1; i += nt)
+        for (int p = 0; p < n; ++p)
+          if (p != r) ll_put(A.ll_push[p], i, ll_pack8(a2a ? send + (long long)p * A.total : send, i, A.bytes), flag);
+    } else if (b == 0 && tid == 0) {
+      for (int p = 0; p < n; ++p)
+        if (p != r) ll_put(A.ll_push[p], 0, 0, flag);  // token: "I am in this launch"
+    }
+    if (!bc) {  // my own block (skipped in place)
+      const char* own = a2a ? send + (long long)r * A.total : send;
+      char* dst = recv + (long long)r * A.total;
+      if (own != dst) block_copy(dst + lo, own + lo, len);
+    }
+    __syncthreads();  // IN_PLACE Alltoall: this slice of my blocks is read before peers' bytes land on it
+    bool ok = true;
+    const uint64_t t0 = wall_clock64();
+    for (int p = 0; p < n && ok; ++p) {
+      if (p == r) continue;
+      const char* in = A.ll_in + (long long)p * A.ll_stride;
+      uint64_t d;
+      if (!bc || p == A.root) {
+        char* dst = bc ? recv : recv + (long long)p * A.total;
+        for (long long i = l0 + tid; i < l1 && ok; i += nt) {
+          ok = ll_get(in, i, flag, t0, pv.timeout_ticks, &d);
+          if (ok) ll_store8(dst, i, A.bytes, d);
+        }
+      } else if (b == 0 && tid == 0) {
+        ok = ll_get(in, 0, flag, t0, pv.timeout_ticks, &d);
+      }
+    }
+    if (!ok) __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return 0;
   }
   if (A.mode == C_BCAST) {

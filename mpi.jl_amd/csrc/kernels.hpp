@@ -303,7 +303,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     return ab;
   }
 
-  if (A.mode == M_AR_LL) {
+  if (A.mode == M_AR_LL || A.mode == M_RED_LL) {
     // small Allreduce in one step: every rank's slice b arrives as LL lines
     // in my own memory (device.hpp ll_exchange), unpacked into my arena slot
     // of its rank; the fold then reads local HBM only, with the same
@@ -314,7 +314,8 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     if (!ll_exchange(A.zc_recv, A.ll_in, A.ll_stride, A.ll_flag, send, bytes, l0, l1, (char*)mine, A.slot_bytes,
                      pv.n, pv.rank, pv.timeout_ticks, pv.err))
       return 0;
-    fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
+    if (A.mode == M_AR_LL || pv.rank == A.root)
+      fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
     return 0;
   }
 
@@ -567,8 +568,17 @@ __device__ __forceinline__ int scan_body(const ScanArgs& A);
 
 template <class OP, class T>
 __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs A) {
-  const int ab = scan_body<OP, T>(A);
-  signal_done(A.pv, ab);
+  // src[] / ll_push[] are indexed by rank at run time: staged in LDS like
+  // FoldArgs (from the kernarg segment the compiler copied the whole block to
+  // scratch in every thread)
+  __shared__ ScanArgs sA;
+  static_assert(sizeof(ScanArgs) % 4 == 0, "ScanArgs word copy");
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&A);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
+  for (unsigned i = threadIdx.x; i < sizeof(ScanArgs) / 4; i += blockDim.x) d[i] = w[i];
+  __syncthreads();
+  const int ab = scan_body<OP, T>(sA);
+  signal_done(sA.pv, ab);
 }
 
 template <class OP, class T>
@@ -579,7 +589,16 @@ __device__ __forceinline__ int scan_body(const ScanArgs& A) {  // returns the ab
   const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
   uint64_t ep = pv.epoch;
   int ab = 0;
-  if (A.zc) {
+  if (A.ll) {
+    // small messages: every rank's slice b arrives as LL lines (device.hpp
+    // ll_exchange; every rank sends to every rank so the area parities stay
+    // safe), unpacked into my arena slots = src[]; no barrier at all
+    const long long es = A.esize, bytes = A.count * es;
+    const long long l0 = (lo * es) / 8, l1 = hi > lo ? (hi * es + 7) / 8 : l0;
+    if (!ll_exchange(A.ll_push, A.ll_in, A.ll_stride, A.ll_flag, (const char*)A.send, bytes, l0, l1,
+                     pv.stage[pv.rank], A.ll_ustride, pv.n, pv.rank, pv.timeout_ticks, pv.err))
+      return 0;
+  } else if (A.zc) {
     // zero-copy (out of place only): the operands are the ranks' sendbufs
     if (!zc_enter(pv, ep++, &ab)) return 0;
   } else {
@@ -609,6 +628,7 @@ __device__ __forceinline__ int scan_body(const ScanArgs& A) {  // returns the ab
       recv[e] = r.x[0];
     }
   }
+  if (A.ll) return 0;
   rank_barrier(pv, ep++, &ab);
   return ab;
 }

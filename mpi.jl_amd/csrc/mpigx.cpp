@@ -747,6 +747,36 @@ int allreduce_ring(mpigx_comm* c, const ZcLaunch& z, long long count, const Type
 }
 
 // Shared driver for Allreduce / Reduce.
+// LL exchange (device.hpp ll_exchange) for a `bytes`-byte message: taken by
+// small Allreduce / Reduce / Scan / Exscan unless MPIGX_ALGO forces the
+// staged one-/two-shot.  The decision is identical on every rank (same count,
+// thresholds that init checked to agree, same environment).
+bool ll_take(mpigx_comm* c, long long bytes) {
+  const char* algo = getenv("MPIGX_ALGO");
+  return c->ll && bytes <= c->ll_max && (long long)c->n * rup(c->ll_max, 16) <= (long long)c->stage_bytes &&
+         !(algo && (!strcmp(algo, "oneshot") || !strcmp(algo, "twoshot")));
+}
+// This launch's LL pointers: push[p] = rank p's area (parity) at my sender
+// slot, *in = my own area (parity), and a flag no earlier launch of the same
+// parity used (the epoch is monotone and equal on every rank).
+void ll_fill(mpigx_comm* c, char** push, const char** in, long long* stride, unsigned* flag) {
+  const long long par = (long long)(c->ll_seq & 1) * kMaxRanks * c->ll_stride;
+  for (int p = 0; p < c->n; ++p) push[p] = c->peer_ll[p] + par + (long long)c->rank * c->ll_stride;
+  *in = c->ll + par;
+  *stride = c->ll_stride;
+  *flag = (unsigned)(c->epoch & 0x7fffffffu) | 0x80000000u;
+}
+void ll_launched(mpigx_comm* c) {
+  c->epoch += 1;
+  c->ll_seq += 1;
+}
+// Bcast / Allgather / Alltoall: LL for blocks up to MPIGX_LL_MAX bytes
+// (MPIGX_ALGO=oneshot/twoshot keeps the staged copy, as for the reductions)
+bool copy_ll_take(mpigx_comm* c, long long bytes) {
+  const char* algo = getenv("MPIGX_ALGO");
+  return c->ll && bytes <= c->ll_max && !(algo && (!strcmp(algo, "oneshot") || !strcmp(algo, "twoshot")));
+}
+
 int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, const TypeInfo* t,
                   int oc, int root, bool all) {
   const int n = c->n, es = t->size;
@@ -803,35 +833,30 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     if (rc || !staged) return rc;
     if (c->zc_require) return MPIGX_ERR_INTERN;
   }
-  // small Allreduce: one LL step (no barrier, kernels.hpp M_AR_LL); the
-  // unpacked contributions take n slots of the arena
-  const long long ustride = rup(c->ll_max, 16);
-  if (all && c->ll && count * es <= c->ll_max && (long long)n * ustride <= (long long)c->stage_bytes &&
-      !(algo_env && (!strcmp(algo_env, "oneshot") || !strcmp(algo_env, "twoshot")))) {
+  // small Allreduce / Reduce: one LL step (no barrier, kernels.hpp M_AR_LL /
+  // M_RED_LL); the unpacked contributions take n slots of my arena
+  if (ll_take(c, count * es)) {
+    const long long ustride = rup(c->ll_max, 16);
     FoldArgs a;
     memset(&a, 0, sizeof a);
     a.pv = make_view(c);
-    a.mode = M_AR_LL;
+    a.mode = all ? M_AR_LL : M_RED_LL;
     a.esize = es;
     a.count = count;
+    a.root = root;
     a.send = send;
     a.recv = recv;
-    const long long par = (long long)(c->ll_seq & 1) * kMaxRanks * c->ll_stride;
-    for (int p = 0; p < n; ++p) a.zc_recv[p] = c->peer_ll[p] + par + (long long)c->rank * c->ll_stride;
-    a.ll_in = c->ll + par;
-    a.ll_stride = c->ll_stride;
-    a.ll_flag = (unsigned)(c->epoch & 0x7fffffffu) | 0x80000000u;
+    ll_fill(c, a.zc_recv, &a.ll_in, &a.ll_stride, &a.ll_flag);
     a.slot_bytes = ustride;
     int nmax, sched;
     const void* ptrs[kMaxRanks];
     for (int p = 0; p < n; ++p) ptrs[p] = c->stage + p * ustride;
-    plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
+    plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
     const int grid = grid_for(c, count * es);
     a.slice = rup(cdiv(count, grid), vec);
     HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
     note_launch(c, a.pv, grid);
-    c->epoch += 1;
-    c->ll_seq += 1;
+    ll_launched(c);
     return finish(c);
   }
   for (long long off = 0; off < count; off += round) {
@@ -1525,6 +1550,25 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
   bool sag = c->n >= 3 && bytes >= c->bcast_sag_min;
   if (env && !strcmp(env, "direct")) sag = false;
   if (env && !strcmp(env, "sag")) sag = c->n >= 2;
+  // (zero-copy first when the size asks for it: tests force it at every size)
+  if (!env && copy_ll_take(c, bytes) && !(c->zc_min > 0 && bytes >= c->zc_min)) {
+    // small: the root's lines straight into every peer's LL area (C_BCAST_LL)
+    CopyArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.mode = C_BCAST_LL;
+    a.root = root;
+    a.bytes = bytes;
+    a.send = buf;
+    a.recv = buf;
+    ll_fill(c, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    const int g = grid_for(c, bytes);
+    a.slice = rup(cdiv(bytes, g), 16);
+    HIPCK(launch_copy(dim3(g), c->stream, a));
+    note_launch(c, a.pv, g);
+    ll_launched(c);
+    return finish(c);
+  }
   if (c->zc_min > 0 && bytes >= c->zc_min) {
     // zero-copy: the non-roots pull straight from the root's buffer (and, for
     // scatter + allgather, from each other's), no copy-in at the root
@@ -1605,6 +1649,24 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
   const char* s = inplace ? (alltoall ? (const char*)recv : (const char*)recv + (long long)r * bytes)
                           : (const char*)send;
   if (n == 1) return copy_n1(c, alltoall ? recv : (char*)recv, s, bytes);
+  if (copy_ll_take(c, bytes) && !(c->zc_min > 0 && bytes * n >= c->zc_min && (!alltoall || !inplace))) {
+    // small: every rank's block(s) as LL lines, unpacked straight into recvbuf
+    CopyArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.mode = alltoall ? C_ALLTOALL_LL : C_ALLGATHER_LL;
+    a.bytes = bytes;
+    a.total = bytes;
+    a.send = s;
+    a.recv = recv;
+    ll_fill(c, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    const int g = grid_for(c, bytes);
+    a.slice = rup(cdiv(bytes, g), 16);
+    HIPCK(launch_copy(dim3(g), c->stream, a));
+    note_launch(c, a.pv, g);
+    ll_launched(c);
+    return finish(c);
+  }
   // large out-of-place Alltoall: pull straight from the peers' sendbufs (no
   // copy-in, no rounds).  IN_PLACE is given by every rank or none (MPI), and
   // (bytes, n, thresholds) agree, so every rank takes the same branch.
@@ -2285,6 +2347,28 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
     });
     if (rc || !staged) return rc;
     if (c->zc_require) return MPIGX_ERR_INTERN;
+  }
+  if (ll_take(c, (long long)count * es)) {
+    // small Scan / Exscan: one LL step, the operands are my arena's unpack
+    // slots (IN_PLACE-safe: my own contribution is copied there too)
+    ScanArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.ll = 1;
+    a.exclusive = exclusive;
+    a.esize = es;
+    a.count = count;
+    const int g = grid_for(c, (long long)count * es);
+    a.slice = rup(cdiv(count, g), vec);
+    a.send = s;
+    a.recv = recvbuf;
+    a.ll_ustride = rup(c->ll_max, 16);
+    for (int p = 0; p < c->n; ++p) a.src[p] = c->stage + p * a.ll_ustride;
+    ll_fill(c, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    HIPCK(L(oc, dim3(g), c->stream, a));
+    note_launch(c, a.pv, g);
+    ll_launched(c);
+    return finish(c);
   }
   long long round = (long long)(c->stage_bytes / es) / vec * vec;
   for (long long off = 0; off < count; off += round) {

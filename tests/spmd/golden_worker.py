@@ -283,6 +283,19 @@ class Runner:
             for inplace in (False, True):
                 got = self.run("allreduce", ins, dt, op, count, inplace=inplace)
                 self.check(same_bits(got, exp, dt == "BFLOAT16"), ("ll", dt, op, count, inplace))
+        # byte movers (C_BCAST_LL / C_ALLGATHER_LL / C_ALLTOALL_LL): ragged byte
+        # counts (partial last line), the 64 KiB limit, every root, IN_PLACE
+        for count in (1, 7, 13, 4097, 65536, 65537):
+            ins = make("UINT8_T", "BXOR", n, count * n, 4300 + count)
+            ins1 = [x[:count] for x in ins]
+            for root in sorted({0, n // 2, n - 1}):
+                got = self.run("bcast", ins1, "UINT8_T", None, count, root=root)
+                self.check(same_bits(got, ins1[root]), ("ll-bcast", root, count))
+            for inplace in (False, True):
+                got = self.run("allgather", ins1, "UINT8_T", None, count, inplace=inplace)
+                self.check(same_bits(got, M.allgather(ins1)[r]), ("ll-allgather", count, inplace))
+                got = self.run("alltoall", ins, "UINT8_T", None, count, inplace=inplace)
+                self.check(same_bits(got, M.alltoall(ins, count)[r]), ("ll-alltoall", count, inplace))
         # send buffer at an odd address (byte lines read bytewise)
         ins = make("UINT8_T", "SUM", n, 1001, 4100)
         raw = dev(np.concatenate([np.zeros(1, np.uint8), ins[r]]))
