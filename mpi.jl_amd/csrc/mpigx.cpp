@@ -647,6 +647,20 @@ int allreduce_push(mpigx_comm* c, const ZcLaunch& z, const void* send, long long
   const int vec = es >= 16 ? 1 : 16 / es;
   long long round = (long long)(c->stage_bytes / es);
   round = (round / (n * (long long)vec)) * n * vec;
+  if (c->ll_unfenced) {
+    // the push writes into the peers' arenas before any barrier, relying on
+    // their previous launch having ended with one; an LL launch does not (a
+    // peer may still be unpacking into its arena), so barrier first.  The
+    // flag follows the same collective sequence on every rank.
+    CopyArgs b;
+    memset(&b, 0, sizeof b);
+    b.pv = make_view(c);
+    b.mode = C_BARRIER;
+    HIPCK(launch_copy(dim3(1), c->stream, b));
+    note_launch(c, b.pv, 1);
+    c->epoch += 1;
+    c->ll_unfenced = false;
+  }
   for (long long off = 0; off < count; off += round) {
     const long long cnt = count - off < round ? count - off : round;
     FoldArgs a;
@@ -769,6 +783,7 @@ void ll_fill(mpigx_comm* c, char** push, const char** in, long long* stride, uns
 void ll_launched(mpigx_comm* c) {
   c->epoch += 1;
   c->ll_seq += 1;
+  c->ll_unfenced = true;
 }
 // Bcast / Allgather / Alltoall: LL for blocks up to MPIGX_LL_MAX bytes
 // (MPIGX_ALGO=oneshot/twoshot keeps the staged copy, as for the reductions)

@@ -129,6 +129,7 @@ struct mpigx_comm {
   long long ll_max = 0;        // MPIGX_LL_MAX: Allreduce bytes that take M_AR_LL (0: off)
   long long ll_stride = 0;     // bytes of one sender's lines (2 x ll_max rounded to 16)
   unsigned long long ll_seq = 0;  // LL launches so far (parity = ll_seq & 1; same on every rank)
+  bool ll_unfenced = false;       // an LL launch (no exit barrier) since the last push two-shot
   unsigned* err = nullptr;  // host-pinned, device-written
   unsigned* err_dev = nullptr;
   // completion counter for blocking calls (host-pinned; kernels add 1 per block)

@@ -320,6 +320,27 @@ class Runner:
         L.mpigx_comm_set_blocking(cv, 1)
         for k, (ins, count, s, d) in enumerate(burst):
             self.check(same_bits(host(d, np.float32), M.allreduce(ins, "FLOAT", "SUM")[r]), ("ll-burst", k, count))
+        if os.environ.get("MPIGX_ZC_MIN"):
+            # LL launches (IN_PLACE Scan keeps LL under the forced zero-copy
+            # threshold) back to back with push two-shots, whose remote stores
+            # into the peers' arenas come before any barrier: the host inserts
+            # one after an LL launch (mpigx.cpp allreduce_push)
+            os.environ["MPIGX_ALGO"] = "push"
+            pairs = []
+            for k in range(12):
+                a = make("INT32_T", "SUM", n, 3000 + k, 4400 + k)
+                b = make("FLOAT", "SUM", n, 5000 + 7 * k, 4500 + k)
+                pairs.append((a, b, dev(a[r]), dev(b[r]), dev(np.zeros((5000 + 7 * k) * 4, np.uint8))))
+            L.mpigx_comm_set_blocking(cv, 0)
+            for a, b, sa, sb, db in pairs:
+                assert L.mpigx_scan(IN_PLACE, P(sa), a[r].size, M.DTYPES["INT32_T"][0], M.OPS["SUM"], cv) == 0
+                assert L.mpigx_allreduce(P(sb), P(db), b[r].size, M.DTYPES["FLOAT"][0], M.OPS["SUM"], cv) == 0
+            assert L.mpigx_comm_synchronize(cv) == 0
+            L.mpigx_comm_set_blocking(cv, 1)
+            os.environ.pop("MPIGX_ALGO", None)
+            for k, (a, b, sa, sb, db) in enumerate(pairs):
+                self.check(same_bits(host(sa, np.int32), M.scan(a, "INT32_T", "SUM")[r]), ("ll-push-scan", k))
+                self.check(same_bits(host(db, np.float32), M.allreduce(b, "FLOAT", "SUM")[r]), ("ll-push-ar", k))
         # the first Bcast (k = 6) spreads root 6 % n's value; later ones re-send it
         self.check(bool((host(bc, np.uint8) == 6 % n).all()), "ll-burst-bcast")
 
