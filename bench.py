@@ -376,6 +376,15 @@ def bench_allreduce(args):
             tw, _ = time_ar(nb, 10, 2)
             sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
         os.environ.pop("MPIGX_ALGO", None)
+    # small messages: the default LL step vs the staged one-shot (2 barriers),
+    # per-call latency in microseconds
+    for nb in (8 << 10, 64 << 10):
+        for algo in (None, "oneshot"):
+            if algo:
+                os.environ["MPIGX_ALGO"] = algo
+            tw, _ = time_ar(nb, 20, 5)
+            sweep[f"{nb >> 10}KiB_{algo or 'll'}_us"] = round(tw * 1e6, 2)
+        os.environ.pop("MPIGX_ALGO", None)
     rings = len(M.ring_strides(n, 4))
     for algo, chans in (("push", 1), ("ring", 1), ("ring", rings)):
         os.environ["MPIGX_ALGO"] = algo
