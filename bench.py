@@ -324,15 +324,39 @@ def bench_allreduce(args):
     correct = check_sample(recv, S // 4, "timed buffers, default algorithm")
     del send, recv
 
+    # Everything below is reported beside the headline.  A section that raises
+    # (on every rank, e.g. an MPI error class returned by a variant) is
+    # recorded and the later sections are skipped, so the headline line is
+    # still printed.
+    errors, alive = {}, [True]
+
+    def guarded(name, fn, default=None):
+        if not alive[0]:
+            errors[name] = "skipped after an earlier failure"
+            return default
+        try:
+            out, bad = fn(), 0.0
+        except Exception as e:  # noqa: BLE001
+            out, bad = default, 1.0
+            errors[name] = f"{type(e).__name__}: {str(e)[:200]}"
+            os.environ.pop("MPIGX_ALGO", None)
+            os.environ.pop("MPIGX_RING_CHANNELS", None)
+        (anybad,) = tmax(bad)
+        if anybad:
+            alive[0] = False
+        return out
+
     # measured xGMI ingress/egress of my GPU over the same workload (SMU
     # metrics, per link, KB; tools/xgmi_counters.py) vs the algorithmic
     # 2S(n-1)/n each way per rank and step
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import xgmi_counters as XC
     bus = torch.cuda.get_device_properties(dev).pci_bus_id
-    xg = None
-    c0 = XC.read(bus)
-    if c0 is not None:
+
+    def xgmi_section():
+        c0 = XC.read(bus)
+        if c0 is None:
+            return None
         reps = max(args.steps, 10)
         xs = rank_input(rank, S // 4)
         xr = torch.empty_like(xs)
@@ -343,76 +367,85 @@ def bench_allreduce(args):
         dist.barrier()
         time.sleep(0.2)  # let the metrics table refresh
         c1 = XC.read(bus)
-        if c1 is not None:
-            rd = sum(b - a for a, b in zip(c0["read_kb"], c1["read_kb"])) * 1024 / reps
-            wr = sum(b - a for a, b in zip(c0["write_kb"], c1["write_kb"])) * 1024 / reps
-            algo_x = 2 * S * (n - 1) / n
-            xg = {"read_bytes_per_step": rd, "write_bytes_per_step": wr, "algorithmic_bytes_per_step": algo_x,
-                  "read_over_algorithmic": round(rd / algo_x, 4), "source": "amd-smi gpu_metrics xgmi_*_data_acc",
-                  "steps": reps}
-        del xs, xr
+        if c1 is None:
+            return None
+        rd = sum(b - a for a, b in zip(c0["read_kb"], c1["read_kb"])) * 1024 / reps
+        wr = sum(b - a for a, b in zip(c0["write_kb"], c1["write_kb"])) * 1024 / reps
+        algo_x = 2 * S * (n - 1) / n
+        return {"read_bytes_per_step": rd, "write_bytes_per_step": wr, "algorithmic_bytes_per_step": algo_x,
+                "read_over_algorithmic": round(rd / algo_x, 4), "source": "amd-smi gpu_metrics xgmi_*_data_acc",
+                "steps": reps}
+    xg = guarded("xgmi_counters", xgmi_section)
 
     # measured xGMI: every rank pulls 64 MiB from every peer at once / from one peer
-    probe = {}
-    for kind, name in ((0, "all_peers"), (1, "one_link")):
-        secs = ctypes.c_double(0)
-        pb = 64 << 20
-        MPI.lib().mpigx_comm_probe(comm.val, kind, pb, ctypes.byref(secs))  # warm
-        MPI.lib().mpigx_comm_probe(comm.val, kind, pb, ctypes.byref(secs))
-        (sec,) = tmax(secs.value)
-        probe[name + "_GBps"] = round(pb * ((n - 1) if kind == 0 else 1) / sec / 1e9, 1)
+    def probe_section():
+        probe = {}
+        for kind, name in ((0, "all_peers"), (1, "one_link")):
+            secs = ctypes.c_double(0)
+            pb = 64 << 20
+            for _ in range(2):  # warm, then timed
+                rc = MPI.lib().mpigx_comm_probe(comm.val, kind, pb, ctypes.byref(secs))
+                if rc:
+                    raise RuntimeError(f"mpigx_comm_probe returned {rc}")
+            (sec,) = tmax(secs.value)
+            probe[name + "_GBps"] = round(pb * ((n - 1) if kind == 0 else 1) / sec / 1e9, 1)
+        return probe
+    probe = guarded("xgmi_probe", probe_section, {})
 
     # size sweep (mpigx), algorithm variants, the ring (MPIGX_ALGO=ring, one
     # ring / every coprime-stride ring) and the RCCL comparison point
     sweep, rccl = {}, {}
     sizes = [8 << 10, 1 << 20, 16 << 20, 64 << 20, S, 1 << 30]
-    for nb in sizes:
-        tw, tk = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
-        sweep[f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"] = {
-            "busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1), "ms": round(tw * 1e3, 4)}
-    for nb in (1 << 20, 16 << 20):
-        for algo in ("oneshot", "twoshot"):
-            os.environ["MPIGX_ALGO"] = algo
-            tw, _ = time_ar(nb, 10, 2)
-            sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
-        os.environ.pop("MPIGX_ALGO", None)
-    # small messages: the default LL step vs the staged one-shot (2 barriers),
-    # per-call latency in microseconds
-    for nb in (8 << 10, 64 << 10):
-        for algo in (None, "oneshot"):
-            if algo:
+    def sweep_section():
+        for nb in sizes:
+            tw, tk = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
+            sweep[f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"] = {
+                "busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1), "ms": round(tw * 1e3, 4)}
+        for nb in (1 << 20, 16 << 20):
+            for algo in ("oneshot", "twoshot"):
                 os.environ["MPIGX_ALGO"] = algo
-            tw, _ = time_ar(nb, 20, 5)
-            sweep[f"{nb >> 10}KiB_{algo or 'll'}_us"] = round(tw * 1e6, 2)
+                tw, _ = time_ar(nb, 10, 2)
+                sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
+            os.environ.pop("MPIGX_ALGO", None)
+        # small messages: the default LL step vs the staged one-shot (2 barriers),
+        # per-call latency in microseconds
+        for nb in (8 << 10, 64 << 10):
+            for algo in ("ll", "oneshot"):
+                os.environ["MPIGX_ALGO"] = algo
+                tw, _ = time_ar(nb, 20, 5)
+                sweep[f"{nb >> 10}KiB_{algo}_us"] = round(tw * 1e6, 2)
+            os.environ.pop("MPIGX_ALGO", None)
+        rings = len(M.ring_strides(n, 4))
+        for algo, chans in (("push", 1), ("ring", 1), ("ring", rings)):
+            os.environ["MPIGX_ALGO"] = algo
+            os.environ["MPIGX_RING_CHANNELS"] = str(chans)
+            tag = algo if algo == "push" or chans == 1 else f"ring{chans}"
+            for nb in (16 << 20, S, 1 << 30):
+                tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
+                sweep[f"{nb >> 20}MiB_{tag}"] = round(busbw(nb, tw), 1)
+            # the variant's timed output, checked like the default's
+            _, _, s_, r_ = time_ar(S, 1, 1, keep=True)
+            sweep[f"{tag}_correct"] = check_sample(r_, S // 4, f"{tag} timed buffers")["sample_bit_exact_vs_oracle"] \
+                if algo == "push" else _ring_check(M, np, r_, S // 4, n, rank_input, tmax, chans)
+            del s_, r_
         os.environ.pop("MPIGX_ALGO", None)
-    rings = len(M.ring_strides(n, 4))
-    for algo, chans in (("push", 1), ("ring", 1), ("ring", rings)):
-        os.environ["MPIGX_ALGO"] = algo
-        os.environ["MPIGX_RING_CHANNELS"] = str(chans)
-        tag = algo if algo == "push" or chans == 1 else f"ring{chans}"
-        for nb in (16 << 20, S, 1 << 30):
-            tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
-            sweep[f"{nb >> 20}MiB_{tag}"] = round(busbw(nb, tw), 1)
-        # the variant's timed output, checked like the default's
-        _, _, s_, r_ = time_ar(S, 1, 1, keep=True)
-        sweep[f"{tag}_correct"] = check_sample(r_, S // 4, f"{tag} timed buffers")["sample_bit_exact_vs_oracle"] \
-            if algo == "push" else _ring_check(M, np, r_, S // 4, n, rank_input, tmax, chans)
-        del s_, r_
-    os.environ.pop("MPIGX_ALGO", None)
-    os.environ.pop("MPIGX_RING_CHANNELS", None)
-    if args.no_rccl:
-        rccl = {"skipped": True}
-    elif same_device:
-        rccl = {"skipped": "ranks share one GPU (RCCL needs one GPU per rank)"}
-    else:
-        try:
-            ng = dist.new_group(backend="nccl")
-            for nb in sizes:
-                tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2,
-                                fn=lambda s_, r_: (r_.copy_(s_), dist.all_reduce(r_, group=ng)))
-                rccl[f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"] = round(busbw(nb, tw), 1)
-        except Exception as e:  # noqa: BLE001
-            rccl = {"error": str(e)[:200]}
+        os.environ.pop("MPIGX_RING_CHANNELS", None)
+    guarded("sweep", sweep_section)
+    def rccl_section():
+        if args.no_rccl:
+            rccl["skipped"] = True
+        elif same_device:
+            rccl["skipped"] = "ranks share one GPU (RCCL needs one GPU per rank)"
+        else:
+            try:
+                ng = dist.new_group(backend="nccl")
+                for nb in sizes:
+                    tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2,
+                                    fn=lambda s_, r_: (r_.copy_(s_), dist.all_reduce(r_, group=ng)))
+                    rccl[f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"] = round(busbw(nb, tw), 1)
+            except Exception as e:  # noqa: BLE001
+                rccl["error"] = str(e)[:200]
+    guarded("rccl", rccl_section)
 
     def time_call(call, steps, warmup):
         for _ in range(warmup):
@@ -430,68 +463,72 @@ def bench_allreduce(args):
     # for Bcast, total recv for Allgather, total send for Alltoall); busbw
     # factors as nccl-tests: 1, (n-1)/n, (n-1)/n
     cfg4 = {}
-    if not args.no_extra:
-        for nb in (64 << 10, 1 << 20, 16 << 20, 128 << 20, 512 << 20):
-            cnt = nb // 4
-            steps = 10 if nb <= (16 << 20) else 3
-            buf = torch.full((cnt,), float(rank), device=dev)
-            tb = time_call(lambda: MPI.Bcast_(buf, 0, comm), steps, 2)
-            okb = bool(torch.all(buf == 0).item())
-            per = cnt // n
-            src = torch.full((per,), float(rank), device=dev)
-            dst = torch.empty(per * n, device=dev)
-            tg = time_call(lambda: MPI.Allgather_(src, dst, per, comm), steps, 2)
-            okg = bool(torch.equal(dst, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per)))
-            a2s = torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) + 100 * rank
-            a2r = torch.empty_like(a2s)
-            ta = time_call(lambda: MPI.Alltoall_(a2s, a2r, per, comm), steps, 2)
-            oka = bool(torch.equal(a2r, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) * 100
-                                   + rank))
-            f = (n - 1) / n
-            (bad,) = tmax(0.0 if (okb and okg and oka) else 1.0)
-            cfg4[f"{nb >> 10}KiB"] = {
-                "bcast_busbw": round(nb / tb / 1e9, 2), "allgather_busbw": round(nb / tg / 1e9 * f, 2),
-                "alltoall_busbw": round(nb / ta / 1e9 * f, 2), "ok": bad == 0.0}
-            del buf, src, dst, a2s, a2r
+    def config4_section():
+        if not args.no_extra:
+            for nb in (64 << 10, 1 << 20, 16 << 20, 128 << 20, 512 << 20):
+                cnt = nb // 4
+                steps = 10 if nb <= (16 << 20) else 3
+                buf = torch.full((cnt,), float(rank), device=dev)
+                tb = time_call(lambda: MPI.Bcast_(buf, 0, comm), steps, 2)
+                okb = bool(torch.all(buf == 0).item())
+                per = cnt // n
+                src = torch.full((per,), float(rank), device=dev)
+                dst = torch.empty(per * n, device=dev)
+                tg = time_call(lambda: MPI.Allgather_(src, dst, per, comm), steps, 2)
+                okg = bool(torch.equal(dst, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per)))
+                a2s = torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) + 100 * rank
+                a2r = torch.empty_like(a2s)
+                ta = time_call(lambda: MPI.Alltoall_(a2s, a2r, per, comm), steps, 2)
+                oka = bool(torch.equal(a2r, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) * 100
+                                       + rank))
+                f = (n - 1) / n
+                (bad,) = tmax(0.0 if (okb and okg and oka) else 1.0)
+                cfg4[f"{nb >> 10}KiB"] = {
+                    "bcast_busbw": round(nb / tb / 1e9, 2), "allgather_busbw": round(nb / tg / 1e9 * f, 2),
+                    "alltoall_busbw": round(nb / ta / 1e9 * f, 2), "ok": bad == 0.0}
+                del buf, src, dst, a2s, a2r
+    guarded("config4", config4_section)
 
     # config 5: Scan! / Exscan! / Reduce! with BAND/BOR/MAX on Int32/Int64,
     # bit-exact against the fold of every rank's (regenerated) input
-    cfg5, cfg5_ok = {}, True
-    if not args.no_extra:
-        ops = (("BAND", MPI.BAND, torch.bitwise_and), ("BOR", MPI.BOR, torch.bitwise_or),
-               ("MAX", MPI.MAX, torch.maximum))
-        for tdt, lim in ((torch.int32, 1 << 31), (torch.int64, 1 << 62)):
-            for cnt in (1 << 10, 1 << 20, 64 << 20):
-                def gen(q):
-                    g = torch.Generator(device=dev).manual_seed(7000 + 31 * q + cnt)
-                    return torch.randint(-lim, lim, (cnt,), dtype=tdt, device=dev, generator=g)
-                xs = [gen(q) for q in range(n)]
-                mine = xs[rank]
-                for oname, op, fn in ops:
-                    pref = [xs[0]]
-                    for q in range(1, n):
-                        pref.append(fn(pref[-1], xs[q]))
-                    out = torch.zeros_like(mine)
-                    steps = 3 if cnt >= (64 << 20) else 5
-                    res = {}
-                    ts = time_call(lambda: MPI.Scan_(mine, out, op, comm), steps, 1)
-                    ok = bool(torch.equal(out, pref[rank]))
-                    res["scan_algbw"] = round(cnt * mine.element_size() / ts / 1e9, 2)
-                    out.zero_()
-                    te = time_call(lambda: MPI.Exscan_(mine, out, op, comm), steps, 1)
-                    ok &= rank == 0 or bool(torch.equal(out, pref[rank - 1]))
-                    res["exscan_algbw"] = round(cnt * mine.element_size() / te / 1e9, 2)
-                    root = n - 1
-                    rout = torch.zeros_like(mine) if rank == root else None
-                    tr = time_call(lambda: MPI.Reduce_(mine, rout, op, root, comm), steps, 1)
-                    if rank == root:
-                        ok &= bool(torch.equal(rout, pref[-1]))
-                    res["reduce_algbw"] = round(cnt * mine.element_size() / tr / 1e9, 2)
-                    (bad,) = tmax(0.0 if ok else 1.0)
-                    res["bit_exact"] = bad == 0.0
-                    cfg5_ok &= res["bit_exact"]
-                    cfg5[f"{str(tdt)[6:]}_{oname}_{cnt}"] = res
-                del xs, pref, mine, out
+    cfg5, cfg5_ok = {}, [True]
+    def config5_section():
+        if not args.no_extra:
+            ops = (("BAND", MPI.BAND, torch.bitwise_and), ("BOR", MPI.BOR, torch.bitwise_or),
+                   ("MAX", MPI.MAX, torch.maximum))
+            for tdt, lim in ((torch.int32, 1 << 31), (torch.int64, 1 << 62)):
+                for cnt in (1 << 10, 1 << 20, 64 << 20):
+                    def gen(q):
+                        g = torch.Generator(device=dev).manual_seed(7000 + 31 * q + cnt)
+                        return torch.randint(-lim, lim, (cnt,), dtype=tdt, device=dev, generator=g)
+                    xs = [gen(q) for q in range(n)]
+                    mine = xs[rank]
+                    for oname, op, fn in ops:
+                        pref = [xs[0]]
+                        for q in range(1, n):
+                            pref.append(fn(pref[-1], xs[q]))
+                        out = torch.zeros_like(mine)
+                        steps = 3 if cnt >= (64 << 20) else 5
+                        res = {}
+                        ts = time_call(lambda: MPI.Scan_(mine, out, op, comm), steps, 1)
+                        ok = bool(torch.equal(out, pref[rank]))
+                        res["scan_algbw"] = round(cnt * mine.element_size() / ts / 1e9, 2)
+                        out.zero_()
+                        te = time_call(lambda: MPI.Exscan_(mine, out, op, comm), steps, 1)
+                        ok &= rank == 0 or bool(torch.equal(out, pref[rank - 1]))
+                        res["exscan_algbw"] = round(cnt * mine.element_size() / te / 1e9, 2)
+                        root = n - 1
+                        rout = torch.zeros_like(mine) if rank == root else None
+                        tr = time_call(lambda: MPI.Reduce_(mine, rout, op, root, comm), steps, 1)
+                        if rank == root:
+                            ok &= bool(torch.equal(rout, pref[-1]))
+                        res["reduce_algbw"] = round(cnt * mine.element_size() / tr / 1e9, 2)
+                        (bad,) = tmax(0.0 if ok else 1.0)
+                        res["bit_exact"] = bad == 0.0
+                        cfg5_ok[0] &= res["bit_exact"]
+                        cfg5[f"{str(tdt)[6:]}_{oname}_{cnt}"] = res
+                    del xs, pref, mine, out
+    guarded("config5", config5_section)
 
     # the reference path on this box's host cores, same run (rank 0 only)
     cpu_ar = None
@@ -534,11 +571,14 @@ def bench_allreduce(args):
             "sweep_mpigx_busbw": sweep,
             "rccl_busbw": rccl,
             "config4_bcast_allgather_alltoall": cfg4,
-            "config5_scan_exscan_reduce": {"bit_exact_all": cfg5_ok, "cases": cfg5},
+            "config5_scan_exscan_reduce": {"bit_exact_all": cfg5_ok[0] and "config5" not in errors, "cases": cfg5},
+            "errors": errors or None,
         }
         print(json.dumps(res), flush=True)
-    MPI.Finalize()
-    dist.destroy_process_group()
+    try:
+        MPI.Finalize()
+    finally:
+        dist.destroy_process_group()
 
 
 def _ring_check(M, np, recv, count, n, rank_input, tmax, nch):

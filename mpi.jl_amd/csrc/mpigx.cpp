@@ -765,10 +765,16 @@ int allreduce_ring(mpigx_comm* c, const ZcLaunch& z, long long count, const Type
 // small Allreduce / Reduce / Scan / Exscan unless MPIGX_ALGO forces the
 // staged one-/two-shot.  The decision is identical on every rank (same count,
 // thresholds that init checked to agree, same environment).
-bool ll_take(mpigx_comm* c, long long bytes) {
+// MPIGX_ALGO=ll takes it up to the area's capacity (MPIGX_LL_MAX), otherwise
+// up to MPIGX_LL_AUTO.
+bool ll_fits(mpigx_comm* c, long long bytes) {
   const char* algo = getenv("MPIGX_ALGO");
-  return c->ll && bytes <= c->ll_max && (long long)c->n * rup(c->ll_max, 16) <= (long long)c->stage_bytes &&
-         !(algo && (!strcmp(algo, "oneshot") || !strcmp(algo, "twoshot")));
+  if (algo && (!strcmp(algo, "oneshot") || !strcmp(algo, "twoshot"))) return false;
+  const bool forced = algo && !strcmp(algo, "ll");
+  return c->ll && bytes <= (forced ? c->ll_max : c->ll_auto);
+}
+bool ll_take(mpigx_comm* c, long long bytes) {
+  return ll_fits(c, bytes) && (long long)c->n * rup(c->ll_max, 16) <= (long long)c->stage_bytes;
 }
 // This launch's LL pointers: push[p] = rank p's area (parity) at my sender
 // slot, *in = my own area (parity), and a flag no earlier launch of the same
@@ -787,10 +793,7 @@ void ll_launched(mpigx_comm* c) {
 }
 // Bcast / Allgather / Alltoall: LL for blocks up to MPIGX_LL_MAX bytes
 // (MPIGX_ALGO=oneshot/twoshot keeps the staged copy, as for the reductions)
-bool copy_ll_take(mpigx_comm* c, long long bytes) {
-  const char* algo = getenv("MPIGX_ALGO");
-  return c->ll && bytes <= c->ll_max && !(algo && (!strcmp(algo, "oneshot") || !strcmp(algo, "twoshot")));
-}
+bool copy_ll_take(mpigx_comm* c, long long bytes) { return ll_fits(c, bytes); }
 
 int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, const TypeInfo* t,
                   int oc, int root, bool all) {
@@ -1235,6 +1238,11 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   if (c->ll_max < 0) c->ll_max = 0;
   if (c->ll_max > (4ll << 20)) c->ll_max = 4ll << 20;
   c->ll_stride = rup(c->ll_max, 16) / 8 * kLLLine;
+  // default LL range: 16 KiB — on ranks sharing one GPU the LL step beat the
+  // staged one-shot at 8 B but not at 64 KiB (profiles/r02_latency_*); the
+  // N>1 bench line measures both at 8 and 64 KiB (MPIGX_ALGO=ll forces LL)
+  c->ll_auto = env_ll("MPIGX_LL_AUTO", 16 << 10);
+  if (c->ll_auto > c->ll_max) c->ll_auto = c->ll_max;
   if (c->ll_max > 0 && nranks > 1) {
     const size_t llb = (size_t)2 * kMaxRanks * c->ll_stride;
     HIPCK(hipExtMallocWithFlags((void**)&c->ll, llb, hipDeviceMallocUncached));

@@ -126,7 +126,8 @@ struct mpigx_comm {
   size_t stage_bytes = 0;
   uint64_t* sig = nullptr;
   char* ll = nullptr;          // LL area (uncached): [2 parities][kMaxRanks senders][ll_stride]
-  long long ll_max = 0;        // MPIGX_LL_MAX: Allreduce bytes that take M_AR_LL (0: off)
+  long long ll_max = 0;        // MPIGX_LL_MAX: LL capacity per sender (bytes; 0: no LL area)
+  long long ll_auto = 0;       // MPIGX_LL_AUTO: largest message that takes LL by default
   long long ll_stride = 0;     // bytes of one sender's lines (2 x ll_max rounded to 16)
   unsigned long long ll_seq = 0;  // LL launches so far (parity = ll_seq & 1; same on every rank)
   bool ll_unfenced = false;       // an LL launch (no exit barrier) since the last push two-shot

@@ -27,8 +27,8 @@ from oracle import mpich_model as M  # noqa: E402
 IN_PLACE = ctypes.c_void_p(-1 & ((1 << 64) - 1))
 # Allreduce algorithms to run every case through; the push two-shot needs the
 # zero-copy mapping, so it joins when the zero-copy test forces that path
-# "ll": the default choice (M_AR_LL for Allreduce <= MPIGX_LL_MAX, the
-# staged / zero-copy algorithms above it); "oneshot"/"twoshot" force those
+# "ll": LL up to its capacity (MPIGX_LL_MAX), the default choice above it;
+# "oneshot"/"twoshot" force the staged algorithms
 AR_ALGOS = ("ll", "oneshot", "twoshot") + (("push",) if os.environ.get("MPIGX_ZC_MIN") else ())
 
 
@@ -273,6 +273,7 @@ class Runner:
         LL launches (both area parities reused while peers run ahead) with
         other collectives between them; vs the MPICH-pinned oracle."""
         L, n, r, cv = self.L, self.n, self.r, self.comm.val
+        os.environ["MPIGX_ALGO"] = "ll"  # LL up to the area's capacity (default: MPIGX_LL_AUTO)
         cases = (("UINT8_T", "BXOR", 1), ("UINT8_T", "SUM", 7), ("INT16_T", "MAX", 5), ("FLOAT", "SUM", 2),
                  ("FLOAT", "SUM", 3), ("DOUBLE", "PROD", 9), ("C_FLOAT_COMPLEX", "PROD", 17),
                  ("BFLOAT16", "SUM", 4099), ("INT64_T", "BAND", 1023), ("FLOAT", "MIN", 16384),
@@ -341,6 +342,7 @@ class Runner:
             for k, (a, b, sa, sb, db) in enumerate(pairs):
                 self.check(same_bits(host(sa, np.int32), M.scan(a, "INT32_T", "SUM")[r]), ("ll-push-scan", k))
                 self.check(same_bits(host(db, np.float32), M.allreduce(b, "FLOAT", "SUM")[r]), ("ll-push-ar", k))
+        os.environ.pop("MPIGX_ALGO", None)
         # the first Bcast (k = 6) spreads root 6 % n's value; later ones re-send it
         self.check(bool((host(bc, np.uint8) == 6 % n).all()), "ll-burst-bcast")
 
