@@ -320,6 +320,15 @@ def bench_allreduce(args):
         return nbytes / t * 2 * (n - 1) / n / 1e9
 
     S = args.mib << 20
+    # the communicator's large-Allreduce tuner (mpigx.cpp ar_tune_*) decides
+    # pull vs push two-shot on its first zero-copy calls: registration, pull,
+    # push.  Those three untimed calls come before the warmup.
+    _ = time_ar(S, 1, 2)
+    ch, pl, ps = ctypes.c_int(-1), ctypes.c_double(0), ctypes.c_double(0)
+    MPI.lib().mpigx_comm_ar_choice(comm.val, ctypes.byref(ch), ctypes.byref(pl), ctypes.byref(ps))
+    ar_tune = {"choice": {-1: "undecided", 0: "pull two-shot", 1: "push two-shot"}[ch.value],
+               "pull_ns_per_MiB": round(pl.value, 1), "push_ns_per_MiB": round(ps.value, 1),
+               "basis": "device time of one 256 MiB call each, max over ranks decides (rank 0's shown)"}
     t, kern, send, recv = time_ar(S, args.steps, args.warmup, keep=True)
     correct = check_sample(recv, S // 4, "timed buffers, default algorithm")
     del send, recv
@@ -567,6 +576,7 @@ def bench_allreduce(args):
             "cpu_baseline": None,
             "cpu_reference_allreduce": cpu_ar,
             "correct": correct,
+            "ar_tune": ar_tune,
             "xgmi_probe": probe,
             "sweep_mpigx_busbw": sweep,
             "rccl_busbw": rccl,

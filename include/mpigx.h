@@ -145,6 +145,11 @@ int mpigx_comm_zc_stats(mpigx_comm_t comm, unsigned long long *optimistic_hits,
 /* Host time of the last collective call from its entry to its first kernel
  * launch (argument checks, planning, zero-copy view resolution).  Diagnostic. */
 int mpigx_comm_host_stats(mpigx_comm_t comm, double *prelaunch_us);
+/* Large (zero-copy-sized) Allreduce algorithm the communicator measured and
+ * chose (MPIGX_AR_TUNE): *choice = -1 undecided, 0 pull two-shot, 1 push
+ * two-shot; *pull_ns_per_mib / *push_ns_per_mib = this rank's measured device
+ * time per MiB of message (0 = not measured).  Diagnostic. */
+int mpigx_comm_ar_choice(mpigx_comm_t comm, int *choice, double *pull_ns_per_mib, double *push_ns_per_mib);
 
 /* Diagnostic (bench roofline denominator): every rank pulls `bytes` from
  * every peer's staging arena at once (kind 0: aggregate xGMI ingress) or

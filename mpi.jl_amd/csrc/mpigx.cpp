@@ -795,6 +795,45 @@ void ll_launched(mpigx_comm* c) {
 // (MPIGX_ALGO=oneshot/twoshot keeps the staged copy, as for the reductions)
 bool copy_ll_take(mpigx_comm* c, long long bytes) { return ll_fits(c, bytes); }
 
+// Large-Allreduce tuner.  Whether pulling peer data over xGMI (two-shot,
+// M_AR_ZC) or pushing it (M_AR_PUSH) moves more bytes per second depends on
+// the fabric, so the communicator measures both on its first zero-copy-sized
+// Allreduces (blocking calls only: the host then knows the launch finished)
+// and keeps the faster.  Device time of the launch, max over ranks (one host
+// exchange), per byte; push must win by 3 % to replace the pull.  Both give
+// the same bits (same fold schedule), so the choice never changes results.
+// Returns the variant to time on this call (0 pull, 1 push) or -1.  Every
+// rank sees the same calls and outcomes (blocking mode, MPIGX_AR_TUNE and the
+// zero-copy verdict agree), so the exchange in ar_tune_note is collective.
+int ar_tune_pick(mpigx_comm* c, bool* push) {
+  if (c->ar_choice >= 0) {
+    *push = c->ar_choice == 1;
+    return -1;
+  }
+  *push = false;
+  if (!c->ar_tune || !c->blocking || c->sync_mode != 1 || !c->ar_ev[0]) return -1;
+  const int step = c->ar_step++;
+  if (step == 0) return -1;  // registration call (host exchange, first imports)
+  *push = step % 2 == 0;     // pull, push, (pull, push ... if a call fell back to staging)
+  return *push ? 1 : 0;
+}
+int ar_tune_note(mpigx_comm* c, int variant, long long bytes) {
+  float ms = 0;
+  // the completion word arrives before the stream reaches the end event
+  HIPCK(hipEventSynchronize(c->ar_ev[1]));
+  HIPCK(hipEventElapsedTime(&ms, c->ar_ev[0], c->ar_ev[1]));
+  c->ar_spb[variant] = (ms / 1e3) / (double)bytes;
+  if (variant != 1 || c->ar_spb[0] <= 0) return MPIGX_SUCCESS;
+  double mine[2] = {c->ar_spb[0], c->ar_spb[1]}, all[kMaxRanks][2];
+  const int rc = host_allgather(c, mine, sizeof mine, all);
+  if (rc) return rc;
+  double w[2] = {0, 0};
+  for (int q = 0; q < c->n; ++q)
+    for (int k = 0; k < 2; ++k) w[k] = all[q][k] > w[k] ? all[q][k] : w[k];
+  c->ar_choice = w[1] < 0.97 * w[0] ? 1 : 0;
+  return MPIGX_SUCCESS;
+}
+
 int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, const TypeInfo* t,
                   int oc, int root, bool all) {
   const int n = c->n, es = t->size;
@@ -807,13 +846,24 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   // count and the thresholds are identical on every rank, so is this test
   if (all && n > 1 && c->zc_min > 0 && count * es >= c->zc_min &&
       !(algo_env && !strcmp(algo_env, "oneshot"))) {
-    const bool push = algo_env && !strcmp(algo_env, "push");
+    bool push = algo_env && !strcmp(algo_env, "push");
     const bool ring = algo_env && !strcmp(algo_env, "ring");
+    // no MPIGX_ALGO: the pull or the push two-shot, whichever measured faster
+    // on this communicator (ar_tune_*); undecided, call 2 times the pull and
+    // call 3 the push (call 1 registers the buffers)
+    const int timed = algo_env ? -1 : ar_tune_pick(c, &push);
     bool staged;
     const int rc = zc_run(c, send, recv, &staged, [&](const ZcLaunch& z) {
       if (ring) return allreduce_ring(c, z, count, t, oc);
-      return push ? allreduce_push(c, z, send, count, t, oc) : allreduce_zc(c, z, count, t, oc);
+      if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
+      const int lr = push ? allreduce_push(c, z, send, count, t, oc) : allreduce_zc(c, z, count, t, oc);
+      if (timed >= 0 && !lr) HIPCK(hipEventRecord(c->ar_ev[1], c->stream));
+      return lr;
     });
+    if (!rc && !staged && timed >= 0) {
+      const int trc = ar_tune_note(c, timed, count * es);
+      if (trc) return trc;
+    }
     if (rc || !staged) return rc;
     if (c->zc_require) return MPIGX_ERR_INTERN;  // tests: the path must not fall back
   }
@@ -1203,6 +1253,8 @@ void comm_release(mpigx_comm* c) {
   if (c->sig) (void)hipFree(c->sig);
   if (c->ll) (void)hipFree(c->ll);
   if (c->dcount_dev) (void)hipFree(c->dcount_dev);
+  for (auto& e : c->ar_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->err) (void)hipHostFree(c->err);
   (void)hipGetLastError();
   delete c;
@@ -1242,6 +1294,13 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   // staged one-shot at 8 B but not at 64 KiB (profiles/r02_latency_*); the
   // N>1 bench line measures both at 8 and 64 KiB (MPIGX_ALGO=ll forces LL)
   c->ll_auto = env_ll("MPIGX_LL_AUTO", 16 << 10);
+  // events of the large-Allreduce tuner (created here, so every rank has them
+  // or, with MPIGX_AR_TUNE=0 on every rank, none does)
+  c->ar_tune = (int)env_ll("MPIGX_AR_TUNE", 1);
+  if (c->ar_tune) {
+    HIPCK(hipEventCreate(&c->ar_ev[0]));
+    HIPCK(hipEventCreate(&c->ar_ev[1]));
+  }
   if (c->ll_auto > c->ll_max) c->ll_auto = c->ll_max;
   if (c->ll_max > 0 && nranks > 1) {
     const size_t llb = (size_t)2 * kMaxRanks * c->ll_stride;
@@ -1500,6 +1559,13 @@ int mpigx_comm_zc_stats(mpigx_comm_t c, unsigned long long* optimistic_hits, uns
 int mpigx_comm_host_stats(mpigx_comm_t c, double* prelaunch_us) {
   if (!c) return MPIGX_ERR_COMM;
   if (prelaunch_us) *prelaunch_us = c->last_prelaunch_s * 1e6;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_ar_choice(mpigx_comm_t c, int* choice, double* pull_ns_per_mib, double* push_ns_per_mib) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (choice) *choice = c->ar_choice;
+  if (pull_ns_per_mib) *pull_ns_per_mib = c->ar_spb[0] * 1e9 * 1048576.0;
+  if (push_ns_per_mib) *push_ns_per_mib = c->ar_spb[1] * 1e9 * 1048576.0;
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_set_reduce_order(mpigx_comm_t c, int order) {

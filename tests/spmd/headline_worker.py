@@ -58,6 +58,19 @@ def main():
     MPI.Allreduce_(send, again, MPI.SUM, comm)
     if not torch.equal(again.view(torch.int32), recv.view(torch.int32)):
         fails.append(("allreduce-repeat",))
+    # the large-Allreduce tuner: call 2 above timed the pull two-shot, call 3
+    # times the push two-shot and decides, call 4 runs the choice; every call
+    # gives the same bits (same fold schedule)
+    import ctypes
+    for k in (3, 4):
+        again.zero_()
+        MPI.Allreduce_(send, again, MPI.SUM, comm)
+        if not torch.equal(again.view(torch.int32), recv.view(torch.int32)):
+            fails.append(("allreduce-tuner-call", k))
+    ch = ctypes.c_int(-2)
+    MPI.lib().mpigx_comm_ar_choice(comm.val, ctypes.byref(ch), None, None)
+    if ch.value not in (0, 1):
+        fails.append(("ar-tune-undecided", ch.value))
     del send, recv, again, xs
 
     # --- Bcast / Allgather / Alltoall at 512 MiB
