@@ -277,6 +277,10 @@ def bench_allreduce(args):
         send = rank_input(rank, count)
         recv = torch.empty_like(send)
         call = (lambda: MPI.Allreduce_(send, recv, MPI.SUM, comm)) if fn is None else (lambda: fn(send, recv))
+        # the communicator's tuners (mpigx.cpp ar_tune_* / mt_*) sample their
+        # candidates on the first calls of a size: untimed, before the warmup
+        for _ in range(8 if fn is None else 0):
+            call()
         for _ in range(warmup):
             call()
         torch.cuda.synchronize()
@@ -321,9 +325,9 @@ def bench_allreduce(args):
 
     S = args.mib << 20
     # the communicator's large-Allreduce tuner (mpigx.cpp ar_tune_*) decides
-    # pull vs push two-shot on its first zero-copy calls: registration, pull,
-    # push.  Those three untimed calls come before the warmup.
-    _ = time_ar(S, 1, 2)
+    # pull vs push two-shot on its first zero-copy calls (registration, pull,
+    # push: time_ar's untimed prelude)
+    _ = time_ar(S, 1, 0)
     ch, pl, ps = ctypes.c_int(-1), ctypes.c_double(0), ctypes.c_double(0)
     MPI.lib().mpigx_comm_ar_choice(comm.val, ctypes.byref(ch), ctypes.byref(pl), ctypes.byref(ps))
     ar_tune = {"choice": {-1: "undecided", 0: "pull two-shot", 1: "push two-shot"}[ch.value],
@@ -440,6 +444,16 @@ def bench_allreduce(args):
         os.environ.pop("MPIGX_ALGO", None)
         os.environ.pop("MPIGX_RING_CHANNELS", None)
     guarded("sweep", sweep_section)
+    # what the small/medium tuner chose per size class of the sweep
+    tune_classes = {}
+    for nb in sorted({8 << 10, 64 << 10, 1 << 20}):
+        k = nb.bit_length() - 1
+        ch, ns = ctypes.c_int(-1), (ctypes.c_double * 3)()
+        MPI.lib().mpigx_comm_tune_class(comm.val, k, ctypes.byref(ch), ns)
+        tune_classes[f"{nb >> 10}KiB"] = {
+            "choice": {-1: "static", 0: "LL", 1: "one-shot", 2: "two-shot"}[ch.value],
+            "ns_per_MiB": {"LL": round(ns[0], 1), "one-shot": round(ns[1], 1), "two-shot": round(ns[2], 1)}}
+
     def rccl_section():
         if args.no_rccl:
             rccl["skipped"] = True
@@ -577,6 +591,7 @@ def bench_allreduce(args):
             "cpu_reference_allreduce": cpu_ar,
             "correct": correct,
             "ar_tune": ar_tune,
+            "tune_classes": tune_classes,
             "xgmi_probe": probe,
             "sweep_mpigx_busbw": sweep,
             "rccl_busbw": rccl,

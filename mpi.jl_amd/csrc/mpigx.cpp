@@ -834,6 +834,78 @@ int ar_tune_note(mpigx_comm* c, int variant, long long bytes) {
   return MPIGX_SUCCESS;
 }
 
+// Small / medium Allreduce tuner (below the zero-copy size).  The LL step,
+// the staged one-shot and the staged two-shot all fold with the same schedule
+// (same bits), and which is fastest at a given size depends on the fabric
+// (xGMI latency vs bytes) — so, like the pull/push choice above, each
+// communicator measures them: per size class k = floor(log2 bytes), the
+// candidates valid for the whole class run twice each in turn on the first
+// calls of that class (device time on the comm stream, min of the two), one
+// host exchange takes the max over ranks, and the class keeps the fastest
+// (another than the static default only if >= 3 % faster).
+enum MidVariant { V_LL = 0, V_ONE = 1, V_TWO = 2 };
+int mt_cands(mpigx_comm* c, int k, int* cand) {
+  const long long lo = 1ll << k, hi = (2ll << k) - 1;
+  int m = 0;
+  if (c->ll && hi <= c->ll_max && (long long)c->n * rup(c->ll_max, 16) <= (long long)c->stage_bytes) cand[m++] = V_LL;
+  if (hi <= (4ll << 20) && hi <= (long long)c->stage_bytes) cand[m++] = V_ONE;
+  if (lo >= (4ll << 10)) cand[m++] = V_TWO;
+  return m;
+}
+// -1: no forced variant (static rules); else the variant to run.  *timed =
+// the variant if this call is a tuning sample, *cls its class.
+int mt_pick(mpigx_comm* c, long long bytes, int* timed, int* cls) {
+  *timed = -1;
+  if (!c->ar_tune || !c->blocking || c->sync_mode != 1 || !c->ar_ev[0] || bytes <= 0) return -1;
+  const int k = 63 - __builtin_clzll((unsigned long long)bytes);
+  if (k >= mpigx_comm::kTuneClasses) return -1;
+  *cls = k;
+  if (c->mt_choice[k] >= 0) return c->mt_choice[k];
+  int cand[3];
+  const int m = mt_cands(c, k, cand);
+  if (m <= 1) return -1;
+  const int s = c->mt_step[k];
+  if (s >= 2 * m) return -1;  // a sample failed: keep the static rules
+  c->mt_step[k] = (unsigned char)(s + 1);
+  *timed = cand[s % m];
+  return *timed;
+}
+int mt_default(mpigx_comm* c, long long bytes) {
+  return ll_take(c, bytes) ? V_LL : bytes <= c->oneshot_max ? V_ONE : V_TWO;
+}
+int mt_note(mpigx_comm* c, int k, int variant, long long bytes) {
+  float ms = 0;
+  HIPCK(hipEventSynchronize(c->ar_ev[1]));
+  HIPCK(hipEventElapsedTime(&ms, c->ar_ev[0], c->ar_ev[1]));
+  const double spb = (ms / 1e3) / (double)bytes;
+  double& best = c->mt_spb[k][variant];
+  if (best <= 0 || spb < best) best = spb;
+  int cand[3];
+  const int m = mt_cands(c, k, cand);
+  if (c->mt_step[k] != 2 * m) return MPIGX_SUCCESS;
+  double all[kMaxRanks][3];
+  const int rc = host_allgather(c, c->mt_spb[k], sizeof(double) * 3, all);
+  if (rc) return rc;
+  double w[3] = {0, 0, 0};
+  for (int q = 0; q < c->n; ++q)
+    for (int v = 0; v < 3; ++v) w[v] = all[q][v] > w[v] ? all[q][v] : w[v];
+  const int def = mt_default(c, 1ll << k);
+  int best_v = -1;
+  for (int i = 0; i < m; ++i)
+    if (w[cand[i]] > 0 && (best_v < 0 || w[cand[i]] < w[best_v])) best_v = cand[i];
+  if (best_v >= 0 && w[def] > 0 && !(w[best_v] < 0.97 * w[def])) best_v = def;
+  c->mt_choice[k] = (signed char)(best_v >= 0 ? best_v : def);
+  return MPIGX_SUCCESS;
+}
+
+// finish() of a call that may be a tuning sample (mt_pick)
+int mt_finish(mpigx_comm* c, int timed, int cls, long long bytes) {
+  if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[1], c->stream));
+  int rc = finish(c);
+  if (!rc && timed >= 0) rc = mt_note(c, cls, timed, bytes);
+  return rc;
+}
+
 int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, const TypeInfo* t,
                   int oc, int root, bool all) {
   const int n = c->n, es = t->size;
@@ -901,9 +973,13 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     if (rc || !staged) return rc;
     if (c->zc_require) return MPIGX_ERR_INTERN;
   }
+  // below the zero-copy size: the measured variant for Allreduce (mt_*)
+  int timed = -1, cls = -1;
+  const int force = (all && !algo_env) ? mt_pick(c, count * es, &timed, &cls) : -1;
+  if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
   // small Allreduce / Reduce: one LL step (no barrier, kernels.hpp M_AR_LL /
   // M_RED_LL); the unpacked contributions take n slots of my arena
-  if (ll_take(c, count * es)) {
+  if (force >= 0 ? force == V_LL : ll_take(c, count * es)) {
     const long long ustride = rup(c->ll_max, 16);
     FoldArgs a;
     memset(&a, 0, sizeof a);
@@ -925,7 +1001,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
     note_launch(c, a.pv, grid);
     ll_launched(c);
-    return finish(c);
+    return mt_finish(c, timed, cls, count * es);
   }
   for (long long off = 0; off < count; off += round) {
     const long long cnt = count - off < round ? count - off : round;
@@ -945,6 +1021,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     bool oneshot = cnt * es <= c->oneshot_max;
     if (algo_env && !strcmp(algo_env, "oneshot")) oneshot = true;
     if (algo_env && !strcmp(algo_env, "twoshot")) oneshot = false;
+    if (force == V_ONE || force == V_TWO) oneshot = force == V_ONE;
     int grid, nbar;
     if (oneshot) {
       a.mode = all ? M_AR_ONESHOT : M_RED_ONESHOT;
@@ -962,7 +1039,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     note_launch(c, a.pv, grid);
     c->epoch += nbar;
   }
-  return finish(c);
+  return mt_finish(c, timed, cls, count * es);
 }
 
 int check_comm(mpigx_comm* c) {
@@ -1297,6 +1374,7 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   // events of the large-Allreduce tuner (created here, so every rank has them
   // or, with MPIGX_AR_TUNE=0 on every rank, none does)
   c->ar_tune = (int)env_ll("MPIGX_AR_TUNE", 1);
+  for (auto& x : c->mt_choice) x = -1;
   if (c->ar_tune) {
     HIPCK(hipEventCreate(&c->ar_ev[0]));
     HIPCK(hipEventCreate(&c->ar_ev[1]));
@@ -1566,6 +1644,14 @@ int mpigx_comm_ar_choice(mpigx_comm_t c, int* choice, double* pull_ns_per_mib, d
   if (choice) *choice = c->ar_choice;
   if (pull_ns_per_mib) *pull_ns_per_mib = c->ar_spb[0] * 1e9 * 1048576.0;
   if (push_ns_per_mib) *push_ns_per_mib = c->ar_spb[1] * 1e9 * 1048576.0;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_tune_class(mpigx_comm_t c, int log2_bytes, int* choice, double* ns_per_mib) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (log2_bytes < 0 || log2_bytes >= mpigx_comm::kTuneClasses) return MPIGX_ERR_ARG;
+  if (choice) *choice = c->mt_choice[log2_bytes];
+  if (ns_per_mib)
+    for (int v = 0; v < 3; ++v) ns_per_mib[v] = c->mt_spb[log2_bytes][v] * 1e9 * 1048576.0;
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_set_reduce_order(mpigx_comm_t c, int order) {

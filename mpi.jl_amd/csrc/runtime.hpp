@@ -138,6 +138,12 @@ struct mpigx_comm {
   int ar_step = 0;                // zero-copy Allreduces seen while undecided
   double ar_spb[2] = {0, 0};      // device seconds per byte: pull, push (this rank)
   hipEvent_t ar_ev[2] = {nullptr, nullptr};
+  // small / medium Allreduce tuner (mpigx.cpp mt_*): per size class
+  // (floor(log2 bytes)) the measured choice among LL / one-shot / two-shot
+  static constexpr int kTuneClasses = 40;
+  signed char mt_choice[kTuneClasses];     // -1 undecided
+  unsigned char mt_step[kTuneClasses] = {};
+  double mt_spb[kTuneClasses][3] = {};     // min device seconds per byte per variant (0: none)
   unsigned* err = nullptr;  // host-pinned, device-written
   unsigned* err_dev = nullptr;
   // completion counter for blocking calls (host-pinned; kernels add 1 per block)

@@ -346,6 +346,23 @@ class Runner:
         # the first Bcast (k = 6) spreads root 6 % n's value; later ones re-send it
         self.check(bool((host(bc, np.uint8) == 6 % n).all()), "ll-burst-bcast")
 
+    def tune_cases(self):
+        """The small/medium Allreduce tuner (no MPIGX_ALGO): the first calls of
+        a size class run every candidate (LL / one-shot / two-shot) twice,
+        then the class keeps one; every call must give MPICH's bits."""
+        L, n, r, cv = self.L, self.n, self.r, self.comm.val
+        os.environ.pop("MPIGX_ALGO", None)
+        for k, count in ((12, 1100), (13, 2500), (16, 20000)):  # FLOAT: 4.4 KB, 10 KB, 80 KB
+            assert (count * 4).bit_length() - 1 == k
+            for i in range(8):
+                ins = make("FLOAT", "SUM", n, count + i, 4600 + 10 * k + i)
+                got = self.run("allreduce", ins, "FLOAT", "SUM", count + i, inplace=bool(i % 2))
+                self.check(same_bits(got, M.allreduce(ins, "FLOAT", "SUM")[r]), ("tune", k, i))
+            ch = ctypes.c_int(-2)
+            ns = (ctypes.c_double * 3)()
+            assert L.mpigx_comm_tune_class(cv, k, ctypes.byref(ch), ns) == 0
+            self.check(ch.value in (0, 1, 2), ("tune-decided", k, ch.value))
+
     def ring_cases(self, nchs=(1, 2, 4)):
         """MPIGX_ALGO=ring (zero-copy path): bit-exact against the ring's own
         association (oracle fold_ring, rounds included), and against MPICH:
@@ -407,6 +424,8 @@ def main():
         R.vgolden()
     R.errors()
     R.ll_cases()
+    if not os.environ.get("MPIGX_ZC_MIN"):
+        R.tune_cases()
     R.oracle_cases([("FLOAT", "SUM", 1_000_003), ("DOUBLE", "SUM", 65537), ("FLOAT", "MAX", 100_001),
                     ("INT32_T", "BAND", 262_147), ("INT64_T", "MAX", 50_000), ("BFLOAT16", "SUM", 40_000),
                     ("C_FLOAT_COMPLEX", "PROD", 3333), ("UINT8_T", "BXOR", 100_000)])
