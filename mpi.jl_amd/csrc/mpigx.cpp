@@ -1363,7 +1363,7 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   HIPCK(hipMemset(c->sig, 0, sig_bytes));
   // LL area for small Allreduce (M_AR_LL): uncached like the signal array, so
   // peers' 64-bit line stores and my polls meet in HBM with no cache in between
-  c->ll_max = env_ll("MPIGX_LL_MAX", 64 << 10);
+  c->ll_max = env_ll("MPIGX_LL_MAX", 256 << 10);
   if (c->ll_max < 0) c->ll_max = 0;
   if (c->ll_max > (4ll << 20)) c->ll_max = 4ll << 20;
   c->ll_stride = rup(c->ll_max, 16) / 8 * kLLLine;

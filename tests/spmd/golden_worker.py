@@ -277,7 +277,8 @@ class Runner:
         cases = (("UINT8_T", "BXOR", 1), ("UINT8_T", "SUM", 7), ("INT16_T", "MAX", 5), ("FLOAT", "SUM", 2),
                  ("FLOAT", "SUM", 3), ("DOUBLE", "PROD", 9), ("C_FLOAT_COMPLEX", "PROD", 17),
                  ("BFLOAT16", "SUM", 4099), ("INT64_T", "BAND", 1023), ("FLOAT", "MIN", 16384),
-                 ("FLOAT", "SUM", 16385), ("UINT8_T", "BOR", 65536), ("UINT8_T", "BOR", 65537))
+                 ("FLOAT", "SUM", 16385), ("UINT8_T", "BOR", 65537), ("DOUBLE", "SUM", 32768),
+                 ("UINT8_T", "BOR", 262144), ("UINT8_T", "BOR", 262145))
         for i, (dt, op, count) in enumerate(cases):
             ins = make(dt, op, n, count, 4000 + i, edge=op in ("MAX", "MIN"))
             exp = M.allreduce(ins, dt, op)[r]
@@ -286,7 +287,7 @@ class Runner:
                 self.check(same_bits(got, exp, dt == "BFLOAT16"), ("ll", dt, op, count, inplace))
         # byte movers (C_BCAST_LL / C_ALLGATHER_LL / C_ALLTOALL_LL): ragged byte
         # counts (partial last line), the 64 KiB limit, every root, IN_PLACE
-        for count in (1, 7, 13, 4097, 65536, 65537):
+        for count in (1, 7, 13, 4097, 65537, 262144, 262145):
             ins = make("UINT8_T", "BXOR", n, count * n, 4300 + count)
             ins1 = [x[:count] for x in ins]
             for root in sorted({0, n // 2, n - 1}):
