@@ -446,13 +446,16 @@ def bench_allreduce(args):
     guarded("sweep", sweep_section)
     # what the small/medium tuner chose per size class of the sweep
     tune_classes = {}
-    for nb in sorted({8 << 10, 64 << 10, 1 << 20}):
+
+    def tune_report(kind, name, nb, names, dest):
         k = nb.bit_length() - 1
         ch, ns = ctypes.c_int(-1), (ctypes.c_double * 3)()
-        MPI.lib().mpigx_comm_tune_class(comm.val, k, ctypes.byref(ch), ns)
-        tune_classes[f"{nb >> 10}KiB"] = {
-            "choice": {-1: "static", 0: "LL", 1: "one-shot", 2: "two-shot"}[ch.value],
-            "ns_per_MiB": {"LL": round(ns[0], 1), "one-shot": round(ns[1], 1), "two-shot": round(ns[2], 1)}}
+        MPI.lib().mpigx_comm_tune_class(comm.val, k + 64 * kind, ctypes.byref(ch), ns)
+        dest[f"{name}_{nb >> 10}KiB"] = {
+            "choice": "static" if ch.value < 0 else names[ch.value],
+            "ns_per_MiB": {names[v]: round(ns[v], 1) for v in range(len(names))}}
+    for nb in (8 << 10, 64 << 10, 1 << 20):
+        tune_report(0, "allreduce", nb, ("LL", "one-shot", "two-shot"), tune_classes)
 
     def rccl_section():
         if args.no_rccl:
@@ -470,8 +473,8 @@ def bench_allreduce(args):
                 rccl["error"] = str(e)[:200]
     guarded("rccl", rccl_section)
 
-    def time_call(call, steps, warmup):
-        for _ in range(warmup):
+    def time_call(call, steps, warmup, prelude=0):
+        for _ in range(prelude + warmup):  # prelude: the tuners' sampling calls
             call()
         torch.cuda.synchronize()
         dist.barrier()
@@ -492,16 +495,16 @@ def bench_allreduce(args):
                 cnt = nb // 4
                 steps = 10 if nb <= (16 << 20) else 3
                 buf = torch.full((cnt,), float(rank), device=dev)
-                tb = time_call(lambda: MPI.Bcast_(buf, 0, comm), steps, 2)
+                tb = time_call(lambda: MPI.Bcast_(buf, 0, comm), steps, 2, 6)
                 okb = bool(torch.all(buf == 0).item())
                 per = cnt // n
                 src = torch.full((per,), float(rank), device=dev)
                 dst = torch.empty(per * n, device=dev)
-                tg = time_call(lambda: MPI.Allgather_(src, dst, per, comm), steps, 2)
+                tg = time_call(lambda: MPI.Allgather_(src, dst, per, comm), steps, 2, 6)
                 okg = bool(torch.equal(dst, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per)))
                 a2s = torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) + 100 * rank
                 a2r = torch.empty_like(a2s)
-                ta = time_call(lambda: MPI.Alltoall_(a2s, a2r, per, comm), steps, 2)
+                ta = time_call(lambda: MPI.Alltoall_(a2s, a2r, per, comm), steps, 2, 6)
                 oka = bool(torch.equal(a2r, torch.arange(n, device=dev, dtype=torch.float32).repeat_interleave(per) * 100
                                        + rank))
                 f = (n - 1) / n
@@ -511,6 +514,11 @@ def bench_allreduce(args):
                     "alltoall_busbw": round(nb / ta / 1e9 * f, 2), "ok": bad == 0.0}
                 del buf, src, dst, a2s, a2r
     guarded("config4", config4_section)
+    # the byte movers' tuner at config 4's smallest sizes (per-rank block)
+    tune_classes4 = {}
+    for nb, kinds in (((64 << 10), ((1, "bcast"),)), ((64 << 10) // n, ((2, "allgather"), (3, "alltoall")))):
+        for kind, name in kinds:
+            tune_report(kind, name, nb, ("LL", "staged"), tune_classes4)
 
     # config 5: Scan! / Exscan! / Reduce! with BAND/BOR/MAX on Int32/Int64,
     # bit-exact against the fold of every rank's (regenerated) input
@@ -596,6 +604,7 @@ def bench_allreduce(args):
             "sweep_mpigx_busbw": sweep,
             "rccl_busbw": rccl,
             "config4_bcast_allgather_alltoall": cfg4,
+            "tune_classes_after_config4": tune_classes4,
             "config5_scan_exscan_reduce": {"bit_exact_all": cfg5_ok[0] and "config5" not in errors, "cases": cfg5},
             "errors": errors or None,
         }

@@ -150,11 +150,13 @@ int mpigx_comm_host_stats(mpigx_comm_t comm, double *prelaunch_us);
  * two-shot; *pull_ns_per_mib / *push_ns_per_mib = this rank's measured device
  * time per MiB of message (0 = not measured).  Diagnostic. */
 int mpigx_comm_ar_choice(mpigx_comm_t comm, int *choice, double *pull_ns_per_mib, double *push_ns_per_mib);
-/* Smaller Allreduces (below the zero-copy size), size class log2_bytes =
- * floor(log2(message bytes)): the algorithm the communicator measured and
- * chose (*choice = -1 undecided / not tuned, 0 LL step, 1 staged one-shot,
- * 2 staged two-shot) and this rank's best device time per MiB of each
- * (ns_per_mib[3], 0 = not a candidate or not measured).  Diagnostic. */
+/* Smaller collectives (below the zero-copy size), size class
+ * log2_bytes = floor(log2(message bytes)) + 64 * kind (kind 0 Allreduce,
+ * 1 Bcast, 2 Allgather, 3 Alltoall; the byte movers' class is the per-rank
+ * block): the algorithm the communicator measured and chose (*choice = -1
+ * undecided / not tuned, 0 LL step, 1 staged one-shot (byte movers: the
+ * staged copy), 2 staged two-shot) and this rank's best device time per MiB
+ * of each (ns_per_mib[3], 0 = not a candidate or not measured).  Diagnostic. */
 int mpigx_comm_tune_class(mpigx_comm_t comm, int log2_bytes, int *choice, double *ns_per_mib);
 
 /* Diagnostic (bench roofline denominator): every rank pulls `bytes` from

@@ -843,10 +843,19 @@ int ar_tune_note(mpigx_comm* c, int variant, long long bytes) {
 // calls of that class (device time on the comm stream, min of the two), one
 // host exchange takes the max over ranks, and the class keeps the fastest
 // (another than the static default only if >= 3 % faster).
+// The byte movers (Bcast / Allgather / Alltoall, kinds 1-3) are tuned the
+// same way between their LL step and their staged algorithm (V_ONE), the size
+// class taken from the per-rank block.
 enum MidVariant { V_LL = 0, V_ONE = 1, V_TWO = 2 };
-int mt_cands(mpigx_comm* c, int k, int* cand) {
+enum TuneKind { TK_ALLREDUCE = 0, TK_BCAST = 1, TK_ALLGATHER = 2, TK_ALLTOALL = 3 };
+int mt_cands(mpigx_comm* c, int kind, int k, int* cand) {
   const long long lo = 1ll << k, hi = (2ll << k) - 1;
   int m = 0;
+  if (kind != TK_ALLREDUCE) {
+    if (c->ll && hi <= c->ll_max) cand[m++] = V_LL;
+    cand[m++] = V_ONE;
+    return m;
+  }
   if (c->ll && hi <= c->ll_max && (long long)c->n * rup(c->ll_max, 16) <= (long long)c->stage_bytes) cand[m++] = V_LL;
   if (hi <= (4ll << 20) && hi <= (long long)c->stage_bytes) cand[m++] = V_ONE;
   if (lo >= (4ll << 10)) cand[m++] = V_TWO;
@@ -854,47 +863,51 @@ int mt_cands(mpigx_comm* c, int k, int* cand) {
 }
 // -1: no forced variant (static rules); else the variant to run.  *timed =
 // the variant if this call is a tuning sample, *cls its class.
-int mt_pick(mpigx_comm* c, long long bytes, int* timed, int* cls) {
+int mt_pick(mpigx_comm* c, int kind, long long bytes, int* timed, int* cls) {
   *timed = -1;
   if (!c->ar_tune || !c->blocking || c->sync_mode != 1 || !c->ar_ev[0] || bytes <= 0) return -1;
   const int k = 63 - __builtin_clzll((unsigned long long)bytes);
   if (k >= mpigx_comm::kTuneClasses) return -1;
-  *cls = k;
-  if (c->mt_choice[k] >= 0) return c->mt_choice[k];
+  const int slot = kind * mpigx_comm::kTuneClasses + k;
+  *cls = slot;
+  if (c->mt_choice[slot] >= 0) return c->mt_choice[slot];
   int cand[3];
-  const int m = mt_cands(c, k, cand);
+  const int m = mt_cands(c, kind, k, cand);
   if (m <= 1) return -1;
-  const int s = c->mt_step[k];
+  const int s = c->mt_step[slot];
   if (s >= 2 * m) return -1;  // a sample failed: keep the static rules
-  c->mt_step[k] = (unsigned char)(s + 1);
+  c->mt_step[slot] = (unsigned char)(s + 1);
   *timed = cand[s % m];
   return *timed;
 }
-int mt_default(mpigx_comm* c, long long bytes) {
+bool copy_ll_take(mpigx_comm* c, long long bytes);
+int mt_default(mpigx_comm* c, int kind, long long bytes) {
+  if (kind != TK_ALLREDUCE) return copy_ll_take(c, bytes) ? V_LL : V_ONE;
   return ll_take(c, bytes) ? V_LL : bytes <= c->oneshot_max ? V_ONE : V_TWO;
 }
-int mt_note(mpigx_comm* c, int k, int variant, long long bytes) {
+int mt_note(mpigx_comm* c, int slot, int variant, long long bytes) {
+  const int kind = slot / mpigx_comm::kTuneClasses, k = slot % mpigx_comm::kTuneClasses;
   float ms = 0;
   HIPCK(hipEventSynchronize(c->ar_ev[1]));
   HIPCK(hipEventElapsedTime(&ms, c->ar_ev[0], c->ar_ev[1]));
   const double spb = (ms / 1e3) / (double)bytes;
-  double& best = c->mt_spb[k][variant];
+  double& best = c->mt_spb[slot][variant];
   if (best <= 0 || spb < best) best = spb;
   int cand[3];
-  const int m = mt_cands(c, k, cand);
-  if (c->mt_step[k] != 2 * m) return MPIGX_SUCCESS;
+  const int m = mt_cands(c, kind, k, cand);
+  if (c->mt_step[slot] != 2 * m) return MPIGX_SUCCESS;
   double all[kMaxRanks][3];
-  const int rc = host_allgather(c, c->mt_spb[k], sizeof(double) * 3, all);
+  const int rc = host_allgather(c, c->mt_spb[slot], sizeof(double) * 3, all);
   if (rc) return rc;
   double w[3] = {0, 0, 0};
   for (int q = 0; q < c->n; ++q)
     for (int v = 0; v < 3; ++v) w[v] = all[q][v] > w[v] ? all[q][v] : w[v];
-  const int def = mt_default(c, 1ll << k);
+  const int def = mt_default(c, kind, 1ll << k);
   int best_v = -1;
   for (int i = 0; i < m; ++i)
     if (w[cand[i]] > 0 && (best_v < 0 || w[cand[i]] < w[best_v])) best_v = cand[i];
   if (best_v >= 0 && w[def] > 0 && !(w[best_v] < 0.97 * w[def])) best_v = def;
-  c->mt_choice[k] = (signed char)(best_v >= 0 ? best_v : def);
+  c->mt_choice[slot] = (signed char)(best_v >= 0 ? best_v : def);
   return MPIGX_SUCCESS;
 }
 
@@ -975,7 +988,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   }
   // below the zero-copy size: the measured variant for Allreduce (mt_*)
   int timed = -1, cls = -1;
-  const int force = (all && !algo_env) ? mt_pick(c, count * es, &timed, &cls) : -1;
+  const int force = (all && !algo_env) ? mt_pick(c, TK_ALLREDUCE, count * es, &timed, &cls) : -1;
   if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
   // small Allreduce / Reduce: one LL step (no barrier, kernels.hpp M_AR_LL /
   // M_RED_LL); the unpacked contributions take n slots of my arena
@@ -1648,10 +1661,13 @@ int mpigx_comm_ar_choice(mpigx_comm_t c, int* choice, double* pull_ns_per_mib, d
 }
 int mpigx_comm_tune_class(mpigx_comm_t c, int log2_bytes, int* choice, double* ns_per_mib) {
   if (!c) return MPIGX_ERR_COMM;
-  if (log2_bytes < 0 || log2_bytes >= mpigx_comm::kTuneClasses) return MPIGX_ERR_ARG;
-  if (choice) *choice = c->mt_choice[log2_bytes];
+  // log2_bytes + 64 * kind (0 Allreduce, 1 Bcast, 2 Allgather, 3 Alltoall)
+  const int kind = log2_bytes / 64, k = log2_bytes % 64;
+  if (log2_bytes < 0 || kind >= mpigx_comm::kTuneKinds || k >= mpigx_comm::kTuneClasses) return MPIGX_ERR_ARG;
+  const int slot = kind * mpigx_comm::kTuneClasses + k;
+  if (choice) *choice = c->mt_choice[slot];
   if (ns_per_mib)
-    for (int v = 0; v < 3; ++v) ns_per_mib[v] = c->mt_spb[log2_bytes][v] * 1e9 * 1048576.0;
+    for (int v = 0; v < 3; ++v) ns_per_mib[v] = c->mt_spb[slot][v] * 1e9 * 1048576.0;
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_set_reduce_order(mpigx_comm_t c, int order) {
@@ -1726,7 +1742,12 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
   if (env && !strcmp(env, "direct")) sag = false;
   if (env && !strcmp(env, "sag")) sag = c->n >= 2;
   // (zero-copy first when the size asks for it: tests force it at every size)
-  if (!env && copy_ll_take(c, bytes) && !(c->zc_min > 0 && bytes >= c->zc_min)) {
+  // below the zero-copy size: LL or the staged copy, measured (mt_*)
+  const bool zc_size = c->zc_min > 0 && bytes >= c->zc_min;
+  int timed = -1, cls = -1;
+  const int force = (!env && !getenv("MPIGX_ALGO") && !zc_size) ? mt_pick(c, TK_BCAST, bytes, &timed, &cls) : -1;
+  if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
+  if (force >= 0 ? force == V_LL : (!env && copy_ll_take(c, bytes) && !zc_size)) {
     // small: the root's lines straight into every peer's LL area (C_BCAST_LL)
     CopyArgs a;
     memset(&a, 0, sizeof a);
@@ -1742,7 +1763,7 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
     HIPCK(launch_copy(dim3(g), c->stream, a));
     note_launch(c, a.pv, g);
     ll_launched(c);
-    return finish(c);
+    return mt_finish(c, timed, cls, bytes);
   }
   if (c->zc_min > 0 && bytes >= c->zc_min) {
     // zero-copy: the non-roots pull straight from the root's buffer (and, for
@@ -1800,7 +1821,7 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
     note_launch(c, a.pv, g);
     c->epoch += sag ? 3 : 2;
   }
-  return finish(c);
+  return mt_finish(c, timed, cls, bytes);
 }
 
 static int gather_like(const void* send, int scount, int stype, void* recv, int rcount, int rtype,
@@ -1824,7 +1845,13 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
   const char* s = inplace ? (alltoall ? (const char*)recv : (const char*)recv + (long long)r * bytes)
                           : (const char*)send;
   if (n == 1) return copy_n1(c, alltoall ? recv : (char*)recv, s, bytes);
-  if (copy_ll_take(c, bytes) && !(c->zc_min > 0 && bytes * n >= c->zc_min && (!alltoall || !inplace))) {
+  // below the zero-copy size: LL or the staged copy, measured (mt_*)
+  const bool zc_size = c->zc_min > 0 && bytes * n >= c->zc_min && (!alltoall || !inplace);
+  int timed = -1, cls = -1;
+  const int force = (!getenv("MPIGX_ALGO") && !zc_size)
+                        ? mt_pick(c, alltoall ? TK_ALLTOALL : TK_ALLGATHER, bytes, &timed, &cls) : -1;
+  if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
+  if (force >= 0 ? force == V_LL : (copy_ll_take(c, bytes) && !zc_size)) {
     // small: every rank's block(s) as LL lines, unpacked straight into recvbuf
     CopyArgs a;
     memset(&a, 0, sizeof a);
@@ -1840,7 +1867,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
     HIPCK(launch_copy(dim3(g), c->stream, a));
     note_launch(c, a.pv, g);
     ll_launched(c);
-    return finish(c);
+    return mt_finish(c, timed, cls, bytes);
   }
   // large out-of-place Alltoall: pull straight from the peers' sendbufs (no
   // copy-in, no rounds).  IN_PLACE is given by every rank or none (MPI), and
@@ -1918,7 +1945,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
     note_launch(c, a.pv, g);
     c->epoch += 2;
   }
-  return finish(c);
+  return mt_finish(c, timed, cls, bytes);
 }
 
 // ---------------------------------------------------------------------------

@@ -140,10 +140,13 @@ struct mpigx_comm {
   hipEvent_t ar_ev[2] = {nullptr, nullptr};
   // small / medium Allreduce tuner (mpigx.cpp mt_*): per size class
   // (floor(log2 bytes)) the measured choice among LL / one-shot / two-shot
+  // (kind 0 Allreduce: LL / one-shot / two-shot; kinds 1-3 Bcast / Allgather
+  // / Alltoall: LL / staged), slot = kind * kTuneClasses + class
   static constexpr int kTuneClasses = 40;
-  signed char mt_choice[kTuneClasses];     // -1 undecided
-  unsigned char mt_step[kTuneClasses] = {};
-  double mt_spb[kTuneClasses][3] = {};     // min device seconds per byte per variant (0: none)
+  static constexpr int kTuneKinds = 4;
+  signed char mt_choice[kTuneKinds * kTuneClasses];     // -1 undecided
+  unsigned char mt_step[kTuneKinds * kTuneClasses] = {};
+  double mt_spb[kTuneKinds * kTuneClasses][3] = {};     // min device s/byte per variant (0: none)
   unsigned* err = nullptr;  // host-pinned, device-written
   unsigned* err_dev = nullptr;
   // completion counter for blocking calls (host-pinned; kernels add 1 per block)

@@ -363,6 +363,21 @@ class Runner:
             ns = (ctypes.c_double * 3)()
             assert L.mpigx_comm_tune_class(cv, k, ctypes.byref(ch), ns) == 0
             self.check(ch.value in (0, 1, 2), ("tune-decided", k, ch.value))
+        # the byte movers (kind 1-3: LL vs staged copy), 6 calls per class
+        for k, count in ((11, 3000), (14, 20000)):  # UINT8 blocks: 3 KB, 20 KB
+            for i in range(6):
+                ins = make("UINT8_T", "BXOR", n, (count + i) * n, 4700 + 10 * k + i)
+                ins1 = [x[:count + i] for x in ins]
+                got = self.run("bcast", ins1, "UINT8_T", None, count + i, root=i % n)
+                self.check(same_bits(got, ins1[i % n]), ("tune-bcast", k, i))
+                got = self.run("allgather", ins1, "UINT8_T", None, count + i, inplace=bool(i % 2))
+                self.check(same_bits(got, M.allgather(ins1)[r]), ("tune-allgather", k, i))
+                got = self.run("alltoall", ins, "UINT8_T", None, count + i, inplace=bool(i % 2))
+                self.check(same_bits(got, M.alltoall(ins, count + i)[r]), ("tune-alltoall", k, i))
+            for kind in (1, 2, 3):
+                ch = ctypes.c_int(-2)
+                assert L.mpigx_comm_tune_class(cv, k + 64 * kind, ctypes.byref(ch), None) == 0
+                self.check(ch.value in (0, 1), ("tune-decided-copy", kind, k, ch.value))
 
     def ring_cases(self, nchs=(1, 2, 4)):
         """MPIGX_ALGO=ring (zero-copy path): bit-exact against the ring's own
