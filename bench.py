@@ -420,10 +420,14 @@ def bench_allreduce(args):
                 tw, _ = time_ar(nb, 10, 2)
                 sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
             os.environ.pop("MPIGX_ALGO", None)
-        # small messages: the default LL step vs the staged one-shot (2 barriers),
-        # per-call latency in microseconds
-        for nb in (8 << 10, 64 << 10):
-            for algo in ("ll", "oneshot"):
+        # small / medium messages, every algorithm forced (the LL step, the LL
+        # two-shot, the staged one-/two-shot): per-call latency in microseconds
+        # (where "ll2" does not fit a chunk into half an LL slot it runs the
+        # static choice)
+        for nb in (8 << 10, 64 << 10, 256 << 10, 1 << 20):
+            for algo in ("ll", "ll2", "oneshot", "twoshot"):
+                if algo == "ll" and nb > (256 << 10):
+                    continue  # beyond the LL area's capacity
                 os.environ["MPIGX_ALGO"] = algo
                 tw, _ = time_ar(nb, 20, 5)
                 sweep[f"{nb >> 10}KiB_{algo}_us"] = round(tw * 1e6, 2)
@@ -449,13 +453,13 @@ def bench_allreduce(args):
 
     def tune_report(kind, name, nb, names, dest):
         k = nb.bit_length() - 1
-        ch, ns = ctypes.c_int(-1), (ctypes.c_double * 3)()
+        ch, ns = ctypes.c_int(-1), (ctypes.c_double * 4)()
         MPI.lib().mpigx_comm_tune_class(comm.val, k + 64 * kind, ctypes.byref(ch), ns)
         dest[f"{name}_{nb >> 10}KiB"] = {
             "choice": "static" if ch.value < 0 else names[ch.value],
             "ns_per_MiB": {names[v]: round(ns[v], 1) for v in range(len(names))}}
-    for nb in (8 << 10, 64 << 10, 1 << 20):
-        tune_report(0, "allreduce", nb, ("LL", "one-shot", "two-shot"), tune_classes)
+    for nb in (8 << 10, 64 << 10, 256 << 10, 1 << 20):
+        tune_report(0, "allreduce", nb, ("LL", "one-shot", "two-shot", "LL two-shot"), tune_classes)
 
     def rccl_section():
         if args.no_rccl:

@@ -155,8 +155,9 @@ int mpigx_comm_ar_choice(mpigx_comm_t comm, int *choice, double *pull_ns_per_mib
  * 1 Bcast, 2 Allgather, 3 Alltoall; the byte movers' class is the per-rank
  * block): the algorithm the communicator measured and chose (*choice = -1
  * undecided / not tuned, 0 LL step, 1 staged one-shot (byte movers: the
- * staged copy), 2 staged two-shot) and this rank's best device time per MiB
- * of each (ns_per_mib[3], 0 = not a candidate or not measured).  Diagnostic. */
+ * staged copy), 2 staged two-shot, 3 LL two-shot) and this rank's best device
+ * time per MiB of each (ns_per_mib[4], 0 = not a candidate or not measured).
+ * Diagnostic. */
 int mpigx_comm_tune_class(mpigx_comm_t comm, int log2_bytes, int *choice, double *ns_per_mib);
 
 /* Diagnostic (bench roofline denominator): every rank pulls `bytes` from

@@ -72,6 +72,9 @@ enum FoldMode : int {
                       // peer's lines, unpack them into my arena, fold locally
   M_RED_LL = 9,       // small Reduce: the same exchange (every rank receives from every
                       // rank, which keeps the area parities safe), only the root folds
+  M_AR_LL2 = 10,      // medium Allreduce, two LL exchanges and no barrier: chunk p of
+                      // my sendbuf -> rank p (LL half 0), fold my chunk, my reduced
+                      // chunk -> every rank (LL half 1), unpacked into recvbuf
 };
 
 // LL ("low-latency") lines of M_AR_LL: 16 bytes = two 8-byte halves

@@ -696,6 +696,47 @@ __device__ __forceinline__ bool zc_enter(const PeerView& pv, uint64_t ep, int* a
   return rank_barrier(pv, ep, abort, pv.zc_key, true);
 }
 
+// LL lines of byte messages (common.hpp kLLLine; ll_exchange below):
+// message bytes [8i, 8i+8) of `src` (zero-padded past `bytes`)
+__device__ __forceinline__ uint64_t ll_pack8(const char* src, long long i, long long bytes) {
+  const long long o = 8 * i;
+  if ((((uintptr_t)src) & 7) == 0 && o + 8 <= bytes) return *reinterpret_cast<const uint64_t*>(src + o);
+  uint64_t d = 0;
+  for (int k = 0; k < 8; ++k)
+    if (o + k < bytes) d |= (uint64_t)(uint8_t)src[o + k] << (8 * k);
+  return d;
+}
+__device__ __forceinline__ void ll_put(char* area, long long i, uint64_t d, unsigned flag) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(area + kLLLine * i);
+  const uint64_t fw = (uint64_t)flag << 32;
+  __hip_atomic_store(q, (d & 0xffffffffull) | fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(q + 1, (d >> 32) | fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// waits for line i of a sender's area to carry `flag`; false on timeout
+__device__ __forceinline__ bool ll_get(const char* area, long long i, unsigned flag, uint64_t t0, uint64_t timeout,
+                                       uint64_t* d) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(area + kLLLine * i);
+  for (;;) {
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((unsigned)(a >> 32) == flag && (unsigned)(b >> 32) == flag) {
+      *d = (a & 0xffffffffull) | (b << 32);
+      return true;
+    }
+    if (wall_clock64() - t0 > timeout) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// bytes [8i, 8i+8) ∩ [0, bytes) of dst <- d
+__device__ __forceinline__ void ll_store8(char* dst, long long i, long long bytes, uint64_t d) {
+  const long long o = 8 * i;
+  if ((((uintptr_t)dst) & 7) == 0 && o + 8 <= bytes) {
+    *reinterpret_cast<uint64_t*>(dst + o) = d;
+    return;
+  }
+  for (int k = 0; k < 8 && o + k < bytes; ++k) dst[o + k] = (char)(d >> (8 * k));
+}
+
 // ---------------------------------------------------------------------------
 // LL exchange (M_AR_LL, common.hpp kLLLine) of lines [l0, l1) of a `bytes`-byte
 // message, the block cooperating.  Line i carries message bytes [8i, 8i+8).

@@ -319,6 +319,80 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     return 0;
   }
 
+  if (A.mode == M_AR_LL2) {
+    // LL two-shot (two-shot partition: chunk c, slice b of every chunk per
+    // block).  Lines are chunk-relative; half 0 of every sender slot carries
+    // the reduce-scatter, half 1 the allgather (common.hpp M_AR_LL2).  The
+    // fold reads my own slice from my sendbuf and the peers' from my arena
+    // slots (src[] is chunk-offset on the host, as for the push two-shot).
+    const int n = pv.n, r = pv.rank;
+    const unsigned flag = A.ll_flag;
+    const long long half = A.ll_stride / 2;
+    const uint64_t t0 = wall_clock64();
+    bool ok = true;
+    // chunk c: element offset, bytes, and this block's line range
+    long long lo, hi;  // this block's elements of the chunk (chunk-relative)
+    auto span = [&](int c, long long* c0, long long* cb, long long* l0, long long* l1) {
+      *c0 = lmin((long long)c * A.chunk, A.count);
+      const long long clen = lmin(*c0 + A.chunk, A.count) - *c0;
+      lo = lmin((long long)b * A.slice, clen);
+      hi = lmin(lo + A.slice, clen);
+      *cb = clen * es;
+      *l0 = lo * es / 8;
+      *l1 = hi > lo ? (hi * es + 7) / 8 : *l0;
+    };
+    long long c0, cb, l0, l1;
+    // reduce-scatter: slice b of chunk p -> rank p
+    for (int p = 0; p < n; ++p) {
+      if (p == r) continue;
+      span(p, &c0, &cb, &l0, &l1);
+      for (long long i = l0 + tid; i < l1; i += nt) ll_put(A.zc_recv[p], i, ll_pack8(send + c0 * es, i, cb), flag);
+    }
+    long long r0, rb, rl0, rl1;
+    span(r, &r0, &rb, &rl0, &rl1);
+    const long long rlo = r0 + lo, rhi = r0 + hi;
+    for (int p = 0; p < n && ok; ++p) {
+      if (p == r) continue;
+      for (long long i = rl0 + tid; i < rl1 && ok; i += nt) {
+        uint64_t d;
+        ok = ll_get(A.ll_in + (long long)p * A.ll_stride, i, flag, t0, pv.timeout_ticks, &d);
+        if (ok) *reinterpret_cast<uint64_t*>((char*)mine + (long long)p * A.slot_bytes + 8 * i) = d;
+      }
+    }
+    __syncthreads();
+    if (__syncthreads_or(!ok)) {
+      if (tid == 0) __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return 0;
+    }
+    bool vec = recv_vec;  // my own leaf is my sendbuf: alignment unknown
+#pragma unroll
+    for (int q = 0; q < NMAX; ++q)
+      if (q < A.ntree) vec &= ((uintptr_t)A.src[q] & 15) == 0;
+#pragma unroll
+    for (int q = 0; q < NMAX / 2; ++q)
+      if (q < A.rem) vec &= ((uintptr_t)A.src2[q] & 15) == 0;
+    fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, rlo, rhi, recv, nullptr, vec, tid, nt);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // allgather: my reduced slice -> every rank; slice b of chunk p <- rank p
+    for (long long i = rl0 + tid; i < rl1; i += nt) {
+      const uint64_t d = ll_pack8((const char*)recv + r0 * es, i, rb);
+      for (int p = 0; p < n; ++p)
+        if (p != r) ll_put(A.zc_recv[p] + half, i, d, flag);
+    }
+    for (int p = 0; p < n && ok; ++p) {
+      if (p == r) continue;
+      span(p, &c0, &cb, &l0, &l1);
+      for (long long i = l0 + tid; i < l1 && ok; i += nt) {
+        uint64_t d;
+        ok = ll_get(A.ll_in + (long long)p * A.ll_stride + half, i, flag, t0, pv.timeout_ticks, &d);
+        if (ok) ll_store8((char*)recv + c0 * es, i, cb, d);
+      }
+    }
+    if (!ok) __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return 0;
+  }
+
   if (A.mode == M_AR_ONESHOT || A.mode == M_RED_ONESHOT) {
     const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
     block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);

@@ -846,7 +846,14 @@ int ar_tune_note(mpigx_comm* c, int variant, long long bytes) {
 // The byte movers (Bcast / Allgather / Alltoall, kinds 1-3) are tuned the
 // same way between their LL step and their staged algorithm (V_ONE), the size
 // class taken from the per-rank block.
-enum MidVariant { V_LL = 0, V_ONE = 1, V_TWO = 2 };
+enum MidVariant { V_LL = 0, V_ONE = 1, V_TWO = 2, V_LL2 = 3 };
+// LL two-shot: a chunk (count/n, rounded to vectors) fits half a sender slot
+bool ll2_fits(mpigx_comm* c, long long bytes, int es) {
+  const int vec = es >= 16 ? 1 : 16 / es;
+  const long long chunk = rup(cdiv(bytes / es, c->n), vec) * es;
+  return c->ll && c->n > 1 && chunk <= rup(c->ll_max, 16) / 2 &&
+         (long long)c->n * rup(c->ll_max, 16) <= (long long)c->stage_bytes;
+}
 enum TuneKind { TK_ALLREDUCE = 0, TK_BCAST = 1, TK_ALLGATHER = 2, TK_ALLTOALL = 3 };
 int mt_cands(mpigx_comm* c, int kind, int k, int* cand) {
   const long long lo = 1ll << k, hi = (2ll << k) - 1;
@@ -859,6 +866,10 @@ int mt_cands(mpigx_comm* c, int kind, int k, int* cand) {
   if (c->ll && hi <= c->ll_max && (long long)c->n * rup(c->ll_max, 16) <= (long long)c->stage_bytes) cand[m++] = V_LL;
   if (hi <= (4ll << 20) && hi <= (long long)c->stage_bytes) cand[m++] = V_ONE;
   if (lo >= (4ll << 10)) cand[m++] = V_TWO;
+  // LL two-shot where a whole class's chunk fits (16-B rounding: +16 per rank)
+  if (lo >= (4ll << 10) && c->ll && cdiv(hi, c->n) + 16 <= rup(c->ll_max, 16) / 2 &&
+      (long long)c->n * rup(c->ll_max, 16) <= (long long)c->stage_bytes)
+    cand[m++] = V_LL2;
   return m;
 }
 // -1: no forced variant (static rules); else the variant to run.  *timed =
@@ -871,7 +882,7 @@ int mt_pick(mpigx_comm* c, int kind, long long bytes, int* timed, int* cls) {
   const int slot = kind * mpigx_comm::kTuneClasses + k;
   *cls = slot;
   if (c->mt_choice[slot] >= 0) return c->mt_choice[slot];
-  int cand[3];
+  int cand[4];
   const int m = mt_cands(c, kind, k, cand);
   if (m <= 1) return -1;
   const int s = c->mt_step[slot];
@@ -893,15 +904,15 @@ int mt_note(mpigx_comm* c, int slot, int variant, long long bytes) {
   const double spb = (ms / 1e3) / (double)bytes;
   double& best = c->mt_spb[slot][variant];
   if (best <= 0 || spb < best) best = spb;
-  int cand[3];
+  int cand[4];
   const int m = mt_cands(c, kind, k, cand);
   if (c->mt_step[slot] != 2 * m) return MPIGX_SUCCESS;
-  double all[kMaxRanks][3];
-  const int rc = host_allgather(c, c->mt_spb[slot], sizeof(double) * 3, all);
+  double all[kMaxRanks][4];
+  const int rc = host_allgather(c, c->mt_spb[slot], sizeof(double) * 4, all);
   if (rc) return rc;
-  double w[3] = {0, 0, 0};
+  double w[4] = {0, 0, 0, 0};
   for (int q = 0; q < c->n; ++q)
-    for (int v = 0; v < 3; ++v) w[v] = all[q][v] > w[v] ? all[q][v] : w[v];
+    for (int v = 0; v < 4; ++v) w[v] = all[q][v] > w[v] ? all[q][v] : w[v];
   const int def = mt_default(c, kind, 1ll << k);
   int best_v = -1;
   for (int i = 0; i < m; ++i)
@@ -988,8 +999,38 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   }
   // below the zero-copy size: the measured variant for Allreduce (mt_*)
   int timed = -1, cls = -1;
-  const int force = (all && !algo_env) ? mt_pick(c, TK_ALLREDUCE, count * es, &timed, &cls) : -1;
+  int force = (all && !algo_env) ? mt_pick(c, TK_ALLREDUCE, count * es, &timed, &cls) : -1;
+  if (all && algo_env && !strcmp(algo_env, "ll2")) force = V_LL2;
+  if (force == V_LL2 && !ll2_fits(c, count * es, es)) force = -1;
   if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
+  if (force == V_LL2) {
+    // medium Allreduce: LL two-shot (kernels.hpp M_AR_LL2) — two LL
+    // exchanges, no barrier; the peers' chunk-r slices land in my arena slots
+    const long long ustride = rup(c->ll_max, 16);
+    FoldArgs a;
+    memset(&a, 0, sizeof a);
+    a.pv = make_view(c);
+    a.mode = M_AR_LL2;
+    a.esize = es;
+    a.count = count;
+    a.send = send;
+    a.recv = recv;
+    ll_fill(c, a.zc_recv, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    a.slot_bytes = ustride;
+    a.chunk = rup(cdiv(count, n), vec);
+    const long long c0 = (long long)c->rank * a.chunk < count ? (long long)c->rank * a.chunk : count;
+    int nmax, sched;
+    const void* ptrs[kMaxRanks];
+    for (int q = 0; q < n; ++q)
+      ptrs[q] = q == c->rank ? send : (const void*)(c->stage + q * ustride - c0 * es);
+    plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
+    const int grid = grid_for(c, a.chunk * es);
+    a.slice = rup(cdiv(a.chunk, grid), vec);
+    HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
+    note_launch(c, a.pv, grid);
+    ll_launched(c);
+    return mt_finish(c, timed, cls, count * es);
+  }
   // small Allreduce / Reduce: one LL step (no barrier, kernels.hpp M_AR_LL /
   // M_RED_LL); the unpacked contributions take n slots of my arena
   if (force >= 0 ? force == V_LL : ll_take(c, count * es)) {
@@ -1667,7 +1708,7 @@ int mpigx_comm_tune_class(mpigx_comm_t c, int log2_bytes, int* choice, double* n
   const int slot = kind * mpigx_comm::kTuneClasses + k;
   if (choice) *choice = c->mt_choice[slot];
   if (ns_per_mib)
-    for (int v = 0; v < 3; ++v) ns_per_mib[v] = c->mt_spb[slot][v] * 1e9 * 1048576.0;
+    for (int v = 0; v < 4; ++v) ns_per_mib[v] = c->mt_spb[slot][v] * 1e9 * 1048576.0;
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_set_reduce_order(mpigx_comm_t c, int order) {

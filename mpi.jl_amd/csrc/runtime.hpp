@@ -146,7 +146,7 @@ struct mpigx_comm {
   static constexpr int kTuneKinds = 4;
   signed char mt_choice[kTuneKinds * kTuneClasses];     // -1 undecided
   unsigned char mt_step[kTuneKinds * kTuneClasses] = {};
-  double mt_spb[kTuneKinds * kTuneClasses][3] = {};     // min device s/byte per variant (0: none)
+  double mt_spb[kTuneKinds * kTuneClasses][4] = {};     // min device s/byte per variant (0: none)
   unsigned* err = nullptr;  // host-pinned, device-written
   unsigned* err_dev = nullptr;
   // completion counter for blocking calls (host-pinned; kernels add 1 per block)

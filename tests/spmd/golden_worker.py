@@ -28,8 +28,9 @@ IN_PLACE = ctypes.c_void_p(-1 & ((1 << 64) - 1))
 # Allreduce algorithms to run every case through; the push two-shot needs the
 # zero-copy mapping, so it joins when the zero-copy test forces that path
 # "ll": LL up to its capacity (MPIGX_LL_MAX), the default choice above it;
+# "ll2": the LL two-shot where a chunk fits half an LL slot;
 # "oneshot"/"twoshot" force the staged algorithms
-AR_ALGOS = ("ll", "oneshot", "twoshot") + (("push",) if os.environ.get("MPIGX_ZC_MIN") else ())
+AR_ALGOS = ("ll", "ll2", "oneshot", "twoshot") + (("push",) if os.environ.get("MPIGX_ZC_MIN") else ())
 
 
 def dev(a):
@@ -353,16 +354,16 @@ class Runner:
         then the class keeps one; every call must give MPICH's bits."""
         L, n, r, cv = self.L, self.n, self.r, self.comm.val
         os.environ.pop("MPIGX_ALGO", None)
-        for k, count in ((12, 1100), (13, 2500), (16, 20000)):  # FLOAT: 4.4 KB, 10 KB, 80 KB
+        for k, count in ((12, 1100), (13, 2500), (16, 20000), (18, 70000)):  # FLOAT: 4.4 KB .. 280 KB
             assert (count * 4).bit_length() - 1 == k
-            for i in range(8):
+            for i in range(10):
                 ins = make("FLOAT", "SUM", n, count + i, 4600 + 10 * k + i)
                 got = self.run("allreduce", ins, "FLOAT", "SUM", count + i, inplace=bool(i % 2))
                 self.check(same_bits(got, M.allreduce(ins, "FLOAT", "SUM")[r]), ("tune", k, i))
             ch = ctypes.c_int(-2)
-            ns = (ctypes.c_double * 3)()
+            ns = (ctypes.c_double * 4)()
             assert L.mpigx_comm_tune_class(cv, k, ctypes.byref(ch), ns) == 0
-            self.check(ch.value in (0, 1, 2), ("tune-decided", k, ch.value))
+            self.check(ch.value in (0, 1, 2, 3), ("tune-decided", k, ch.value))
         # the byte movers (kind 1-3: LL vs staged copy), 6 calls per class
         for k, count in ((11, 3000), (14, 20000)):  # UINT8 blocks: 3 KB, 20 KB
             for i in range(6):
