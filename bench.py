@@ -147,21 +147,18 @@ def bench_local(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # the timed K steps carry no instrumentation (value = wall clock)
+    # the timed K steps: wall clock for `value`; HIP events on the launch
+    # stream bracketing the same K back-to-back launches give the kernel's
+    # average launch duration for the roofline (no per-launch instrumentation)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record(stream)
     for _ in range(args.steps):
         step()
+    e1.record(stream)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / args.steps
-    # the kernel's own launch duration for the roofline: HIP events around
-    # each of another K launches on the launch stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for a, b in ev:
-        a.record(stream)
-        step()
-        b.record(stream)
-    torch.cuda.synchronize()
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kern_ms = e0.elapsed_time(e1) / args.steps
     algo = (args.nbuf + 1) * S
 
     # parity spot check of the timed output vs the MPICH-pinned oracle (1 Mi elements)
@@ -228,7 +225,7 @@ def bench_local(args):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "kernel": "fold_local_kernel<OpSum,float,NMAX 8,TREE,SH_FULL,U 4>", "kernel_ms": round(kern_ms, 4),
-                     "achieved_basis": "9 x 256 MiB algorithmic bytes / HIP-event time per launch on the launch stream",
+                     "achieved_basis": "9 x 256 MiB algorithmic bytes / (HIP-event time over the K timed launches on the launch stream / K)",
                      "traffic_basis": "rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE per dispatch (gfx950 FETCH_SIZE "
                                       "halving, MI355X_MICROARCH.md), profiles/r02_traffic.json"},
         "cpu_baseline": cpu,
@@ -249,6 +246,7 @@ def bench_allreduce(args):
     import mpigx as MPI
     from oracle import mpich_model as M
 
+    t_start = time.perf_counter()
     rank = int(os.environ.get("RANK", 0))
     n = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count())
@@ -342,19 +340,23 @@ def bench_allreduce(args):
     # recorded and the later sections are skipped, so the headline line is
     # still printed.
     errors, alive = {}, [True]
+    section_s = {"headline": round(time.perf_counter() - t_start, 2)}  # wall seconds per section (rank 0)
 
     def guarded(name, fn, default=None):
         if not alive[0]:
             errors[name] = "skipped after an earlier failure"
             return default
+        t_sec = time.perf_counter()
         try:
             out, bad = fn(), 0.0
         except Exception as e:  # noqa: BLE001
             out, bad = default, 1.0
             errors[name] = f"{type(e).__name__}: {str(e)[:200]}"
-            os.environ.pop("MPIGX_ALGO", None)
-            os.environ.pop("MPIGX_RING_CHANNELS", None)
         (anybad,) = tmax(bad)
+        section_s[name] = round(time.perf_counter() - t_sec, 2)
+        if not anybad:  # back to the defaults (collective: every rank is here)
+            MPI.set_knob(comm, "ALGO", None)
+            MPI.set_knob(comm, "RING_CHANNELS", 1)
         if anybad:
             alive[0] = False
         return out
@@ -405,6 +407,39 @@ def bench_allreduce(args):
         return probe
     probe = guarded("xgmi_probe", probe_section, {})
 
+    # where the headline call's time goes: per-block phase timestamps of the
+    # kernel (mpigx_comm_set_stamps, 100 MHz device clock) on one more call of
+    # each two-shot variant at the headline size; median over blocks of each
+    # phase, and the span from the first block's entry to the last block's exit
+    def phases_section():
+        out = {}
+        st = torch.zeros(1024 * 8, dtype=torch.int64, device=dev)
+        xs = rank_input(rank, S // 4)
+        xr = torch.empty_like(xs)
+        names = ("entry_barrier", "reduce_scatter", "mid_barrier", "allgather", "exit_barrier")
+        for algo in ("pull", "pull_generic", "push"):
+            MPI.set_knob(comm, "ALGO", algo)
+            for _ in range(2):
+                MPI.Allreduce_(xs, xr, MPI.SUM, comm)
+            st.zero_()
+            MPI.lib().mpigx_comm_set_stamps(comm.val, ctypes.c_void_p(st.data_ptr()))
+            MPI.Allreduce_(xs, xr, MPI.SUM, comm)
+            torch.cuda.synchronize()
+            MPI.lib().mpigx_comm_set_stamps(comm.val, None)
+            t = st.view(1024, 8)[:, :6].cpu().numpy().astype(np.int64)
+            t = t[t[:, 0] > 0]
+            d = np.diff(t, axis=1) / 100.0  # us
+            rec = {nm: round(float(np.median(d[:, k])), 2) for k, nm in enumerate(names)}
+            rec["blocks"] = int(t.shape[0])
+            rec["span_us"] = round(float(t[:, 5].max() - t[:, 0].min()) / 100.0, 2)
+            rec["reduce_scatter_max_us"] = round(float(d[:, 1].max()), 2)
+            rec["allgather_max_us"] = round(float(d[:, 3].max()), 2)
+            out[algo] = rec
+        MPI.set_knob(comm, "ALGO", None)
+        del xs, xr, st
+        return out
+    phases = guarded("phases", phases_section, {})
+
     # size sweep (mpigx), algorithm variants, the ring (MPIGX_ALGO=ring, one
     # ring / every coprime-stride ring) and the RCCL comparison point
     sweep, rccl = {}, {}
@@ -416,10 +451,10 @@ def bench_allreduce(args):
                 "busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1), "ms": round(tw * 1e3, 4)}
         for nb in (1 << 20, 16 << 20):
             for algo in ("oneshot", "twoshot"):
-                os.environ["MPIGX_ALGO"] = algo
+                MPI.set_knob(comm, "ALGO", algo)
                 tw, _ = time_ar(nb, 10, 2)
                 sweep[f"{nb >> 20}MiB_{algo}"] = round(busbw(nb, tw), 1)
-            os.environ.pop("MPIGX_ALGO", None)
+            MPI.set_knob(comm, "ALGO", None)
         # small / medium messages, every algorithm forced (the LL step, the LL
         # two-shot, the staged one-/two-shot): per-call latency in microseconds
         # (where "ll2" does not fit a chunk into half an LL slot it runs the
@@ -428,25 +463,25 @@ def bench_allreduce(args):
             for algo in ("ll", "ll2", "oneshot", "twoshot"):
                 if algo == "ll" and nb > (256 << 10):
                     continue  # beyond the LL area's capacity
-                os.environ["MPIGX_ALGO"] = algo
+                MPI.set_knob(comm, "ALGO", algo)
                 tw, _ = time_ar(nb, 20, 5)
                 sweep[f"{nb >> 10}KiB_{algo}_us"] = round(tw * 1e6, 2)
-            os.environ.pop("MPIGX_ALGO", None)
+            MPI.set_knob(comm, "ALGO", None)
         rings = len(M.ring_strides(n, 4))
-        for algo, chans in (("push", 1), ("ring", 1), ("ring", rings)):
-            os.environ["MPIGX_ALGO"] = algo
-            os.environ["MPIGX_RING_CHANNELS"] = str(chans)
-            tag = algo if algo == "push" or chans == 1 else f"ring{chans}"
+        for algo, chans in (("pull", 1), ("pull_generic", 1), ("push", 1), ("ring", 1), ("ring", rings)):
+            MPI.set_knob(comm, "ALGO", algo)
+            MPI.set_knob(comm, "RING_CHANNELS", chans)
+            tag = algo if algo != "ring" or chans == 1 else f"ring{chans}"
             for nb in (16 << 20, S, 1 << 30):
                 tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
                 sweep[f"{nb >> 20}MiB_{tag}"] = round(busbw(nb, tw), 1)
             # the variant's timed output, checked like the default's
             _, _, s_, r_ = time_ar(S, 1, 1, keep=True)
             sweep[f"{tag}_correct"] = check_sample(r_, S // 4, f"{tag} timed buffers")["sample_bit_exact_vs_oracle"] \
-                if algo == "push" else _ring_check(M, np, r_, S // 4, n, rank_input, tmax, chans)
+                if algo != "ring" else _ring_check(M, np, r_, S // 4, n, rank_input, tmax, chans)
             del s_, r_
-        os.environ.pop("MPIGX_ALGO", None)
-        os.environ.pop("MPIGX_RING_CHANNELS", None)
+        MPI.set_knob(comm, "ALGO", None)
+        MPI.set_knob(comm, "RING_CHANNELS", 1)
     guarded("sweep", sweep_section)
     # what the small/medium tuner chose per size class of the sweep
     tune_classes = {}
@@ -574,7 +609,6 @@ def bench_allreduce(args):
 
     value = busbw(S, t)
     ach = busbw(S, kern)
-    peak_meas = probe.get("all_peers_GBps")
     peak_nom = XGMI_LINK_GBPS * (n - 1)
     if same_device:
         roof = {"bound": "hbm (same-device IPC)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -585,8 +619,8 @@ def bench_allreduce(args):
                 "frac": round(ach / peak_nom, 4),
                 "traffic": xg["read_bytes_per_step"] if xg else None,
                 "peak_basis": f"nominal {n - 1} links x {XGMI_LINK_GBPS} GB/s per direction (MI355X spec)"}
-    roof.update({"peak_probe_GBps": peak_meas, "frac_vs_probe": round(ach / peak_meas, 4) if peak_meas else None,
-                 "probe_basis": "mpigx_comm_probe: every rank pulling 64 MiB from all peers at once",
+    roof.update({"achieved_basis": "busbw of the blocking call's device time (HIP events around each call on the "
+                                   "comm stream), max over ranks",
                  "xgmi_traffic": xg})
     if rank == 0:
         res = {
@@ -604,7 +638,10 @@ def bench_allreduce(args):
             "correct": correct,
             "ar_tune": ar_tune,
             "tune_classes": tune_classes,
-            "xgmi_probe": probe,
+            "xgmi_probe_informational": dict(probe, note="engine's own all-peer / one-link pull of 64 MiB; not a "
+                                                         "peak (it measured below the collective at n=3 in r02)"),
+            "phases_headline_us": phases,
+            "section_wall_s": section_s,
             "sweep_mpigx_busbw": sweep,
             "rccl_busbw": rccl,
             "config4_bcast_allgather_alltoall": cfg4,

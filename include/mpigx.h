@@ -137,6 +137,62 @@ int mpigx_comm_set_stream(mpigx_comm_t comm, void *stream);
 int mpigx_comm_set_blocking(mpigx_comm_t comm, int blocking);
 int mpigx_comm_synchronize(mpigx_comm_t comm);
 int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
+
+/* Path-selecting settings ("knobs").  Each is read ONCE per communicator,
+ * at mpigx_comm_init_rank, from the environment variable named beside it;
+ * init compares every rank's values and fails with MPIGX_ERR_ARG on any
+ * mismatch (a rank launching another kernel than its peers would otherwise
+ * spin until the device timeout).  mpigx_comm_set_knob changes one later: it
+ * is COLLECTIVE (every rank calls it with the same knob and value, in the same
+ * order relative to its other calls on the communicator), checks that over
+ * the control plane, and returns MPIGX_ERR_ARG on every rank, changing
+ * nothing, when they differ.  The two init-only knobs (allocation sizes)
+ * cannot be set. */
+#define MPIGX_KNOB_ALGO 0             /* MPIGX_ALGO: MPIGX_ALGO_* below */
+#define MPIGX_KNOB_BCAST 1            /* MPIGX_BCAST: 0 auto, 1 "direct", 2 "sag" */
+#define MPIGX_KNOB_RING_CHANNELS 2    /* MPIGX_RING_CHANNELS: rings of MPIGX_ALGO_RING (1-4) */
+#define MPIGX_KNOB_MAX_BLOCKS 3       /* MPIGX_MAX_BLOCKS: grid cap of the collective kernels */
+#define MPIGX_KNOB_ONESHOT_MAX 4      /* MPIGX_ONESHOT_MAX: bytes */
+#define MPIGX_KNOB_ZC_MIN 5           /* MPIGX_ZC_MIN: bytes (0: no zero-copy paths) */
+#define MPIGX_KNOB_BCAST_SAG_MIN 6    /* MPIGX_BCAST_SAG_MIN: bytes */
+#define MPIGX_KNOB_ZC_REQUIRE 7       /* MPIGX_ZC_REQUIRE: 1 = error instead of the staged fallback */
+#define MPIGX_KNOB_BYTES_PER_BLOCK 8  /* MPIGX_BYTES_PER_BLOCK */
+#define MPIGX_KNOB_LL_AUTO 9          /* MPIGX_LL_AUTO: bytes (<= MPIGX_LL_MAX) */
+#define MPIGX_KNOB_AR_TUNE 10         /* MPIGX_AR_TUNE: 0/1, the measured algorithm choices */
+#define MPIGX_KNOB_ZC_OPTIMISTIC 11   /* MPIGX_ZC_OPTIMISTIC: 0/1 */
+#define MPIGX_KNOB_SYNC_SPIN 12       /* MPIGX_SYNC_SPIN: 0/1 */
+#define MPIGX_KNOB_STAGING_BYTES 13   /* MPIGX_STAGING_BYTES (init only) */
+#define MPIGX_KNOB_LL_MAX 14          /* MPIGX_LL_MAX (init only) */
+#define MPIGX_KNOB_COUNT 15
+#define MPIGX_ALGO_AUTO 0     /* unset: static rules + the measured choices */
+#define MPIGX_ALGO_LL 1       /* "ll" */
+#define MPIGX_ALGO_LL2 2      /* "ll2" */
+#define MPIGX_ALGO_ONESHOT 3  /* "oneshot" */
+#define MPIGX_ALGO_TWOSHOT 4  /* "twoshot" */
+#define MPIGX_ALGO_PUSH 5     /* "push" */
+#define MPIGX_ALGO_RING 6     /* "ring" */
+#define MPIGX_ALGO_PULL 7     /* "pull": the zero-copy pull two-shot (no pull/push tuning) */
+#define MPIGX_ALGO_PULL_GENERIC 8 /* "pull_generic": the same through the all-modes fold kernel
+                                     (one vector per thread in flight; comparison only) */
+int mpigx_comm_set_knob(mpigx_comm_t comm, int knob, long long value);
+int mpigx_comm_get_knob(mpigx_comm_t comm, int knob, long long *value);
+
+/* Ranks sharing one GPU.  Collective kernels spin on their peers, so every
+ * rank's grid must run at once: init caps MPIGX_KNOB_MAX_BLOCKS so that the
+ * grids of the most-loaded device fit its compute units at the collective
+ * kernels' occupancy, and fails with MPIGX_ERR_OTHER when more than
+ * MPIGX_MAX_RANKS_PER_DEVICE (environment, default 10) ranks share a device
+ * (more rank processes than that did not all get hardware queues at once on
+ * MI355X: some ranks' kernels never started while their peers spun).
+ * *ranks = ranks on the most-loaded device, *cap = the grid cap in force. */
+int mpigx_comm_device_share(mpigx_comm_t comm, int *ranks, int *cap);
+
+/* Diagnostic: per-block phase timestamps of the collective kernels (100 MHz
+ * device wall clock).  stamps = device buffer of >= 1024 x 8 u64 (NULL
+ * disables); slot [block][k]: 0 entry, 1 after the entry barrier, 2 after the
+ * reduce-scatter, 3 after the middle barrier, 4 after the allgather, 5 after
+ * the exit barrier.  Local (not collective). */
+int mpigx_comm_set_stamps(mpigx_comm_t comm, void *stamps);
 /* Zero-copy paths (user buffers mapped by the peers over IPC): how many
  * launches ran on a cached view without any host exchange, and how many
  * host exchanges of buffer registrations there were.  Diagnostic. */

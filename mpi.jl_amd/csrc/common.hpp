@@ -120,6 +120,7 @@ struct PeerView {
   // zero-copy launches (mpigx.cpp zc_run)
   unsigned zc_key;             // id of the buffer-mapping view this launch uses
   int zc_bad;                  // 1: this rank has no valid view (the launch aborts everywhere)
+  unsigned long long* stamps;  // diagnostic phase timestamps [block][8] (null: off)
 };
 
 // Fold-kernel arguments.  Sources/partition are resolved on the host.

@@ -427,4 +427,23 @@ hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a) {
   return hipGetLastError();
 }
 
+// Resident 256-thread blocks per CU of the byte movers that spin on their
+// peers (copy_kernel, vx_kernel) for an nmax (8 or 16); 0 if unknown.
+int occupancy_copy(int nmax) {
+  int a = 0, b = 0;
+  hipError_t e1, e2;
+  if (nmax <= 8) {
+    e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, copy_kernel<8>, kThreads, 0);
+    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, vx_kernel<8>, kThreads, 0);
+  } else {
+    e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, copy_kernel<16>, kThreads, 0);
+    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, vx_kernel<16>, kThreads, 0);
+  }
+  if (e1 != hipSuccess || e2 != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return a < b ? a : b;
+}
+
 }  // namespace mpigx

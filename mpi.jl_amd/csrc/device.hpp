@@ -595,6 +595,83 @@ __device__ __forceinline__ void block_gather(char* const (&dst)[NMAX], const cha
       for (long long j = (len[p] / 16) * 16 + tid; j < len[p]; j += nt) dst[p][j] = src[p][j];
 }
 
+// block_gather with UG 16-B vectors per pair per iteration: UG * m loads in
+// flight per thread before any store (ar_zc_kernel sizes UG so that a thread
+// keeps ~16 loads outstanding at any rank count; with one peer the plain
+// block_gather keeps ONE, which held the n = 2 allgather far below the HBM
+// rate).  Unaligned pairs fall back to block_gather.
+template <int NMAX, int UG>
+__device__ __forceinline__ void block_gather_u(char* const (&dst)[NMAX], const char* const (&src)[NMAX],
+                                               const long long (&len)[NMAX], int m) {
+  bool vec = true;
+  long long nvmax = 0;
+#pragma unroll
+  for (int p = 0; p < NMAX; ++p)
+    if (p < m) {
+      vec &= ((((uintptr_t)dst[p]) | ((uintptr_t)src[p])) & 15) == 0;
+      const long long nv = len[p] / 16;
+      nvmax = nv > nvmax ? nv : nvmax;
+    }
+  if (!vec) {
+    block_gather<NMAX>(dst, src, len, m);
+    return;
+  }
+  const long long tid = threadIdx.x, nt = blockDim.x;
+  for (long long i = tid; i < nvmax; i += UG * nt) {
+    u32x4 v[NMAX][UG];
+#pragma unroll
+    for (int p = 0; p < NMAX; ++p)
+#pragma unroll
+      for (int u = 0; u < UG; ++u)
+        if (p < m && i + u * nt < len[p] / 16) v[p][u] = ld16(src[p] + 16 * (i + u * nt));
+#pragma unroll
+    for (int p = 0; p < NMAX; ++p)
+#pragma unroll
+      for (int u = 0; u < UG; ++u)
+        if (p < m && i + u * nt < len[p] / 16) st16(dst[p] + 16 * (i + u * nt), v[p][u]);
+  }
+#pragma unroll
+  for (int p = 0; p < NMAX; ++p)
+    if (p < m)
+      for (long long j = (len[p] / 16) * 16 + tid; j < len[p]; j += nt) dst[p][j] = src[p][j];
+}
+
+// Fold [lo, hi) into out with U vectors per thread per iteration: all
+// U * (ntree + rem) leaf loads of a thread are issued before any arithmetic
+// (fold_range keeps one vector's leaves in flight).  lo is a multiple of the
+// vector width and every pointer is 16-B aligned (the caller checked).
+template <class OP, class T, int NMAX, int SHAPE, int U>
+__device__ __forceinline__ void fold_span(const FoldArgs& A, const T* const* src, const T* const* src2, long long lo,
+                                          long long hi, T* out) {
+  constexpr int W = VecW<T>::v;
+  const long long tid = threadIdx.x, nt = blockDim.x;
+  const long long nv = (hi - lo) / W;
+  long long v0 = tid;
+  for (; v0 + (long long)(U - 1) * nt < nv; v0 += U * nt) {
+    Leaves<T, NMAX, SHAPE, W> L[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_leaves<T, NMAX, S_TREE, SHAPE, W>(A, src, src2, lo + (v0 + u * nt) * W, L[u]);
+    unsigned strad = 0;  // vectors straddling a Rabenseifner block boundary
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long e = lo + (v0 + u * nt) * W;
+      Vec<T, W> r;
+      if (fold_leaves<OP, T, NMAX, S_TREE, SHAPE, W>(A, e, L[u], r)) stv<T, W>(out + e, r);
+      else strad |= 1u << u;
+    }
+#pragma unroll 1
+    for (int u = 0; u < U; ++u)
+      if ((strad >> u) & 1u) fold_elems<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, lo + (v0 + u * nt) * W, W, out, nullptr);
+  }
+  for (; v0 < nv; v0 += nt) {
+    const long long e = lo + v0 * W;
+    Vec<T, W> r;
+    if (fold_at<OP, T, NMAX, S_TREE, SHAPE, W>(A, src, src2, e, r)) stv<T, W>(out + e, r);
+    else fold_elems<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, e, W, out, nullptr);
+  }
+  for (long long e = lo + nv * W + tid; e < hi; e += nt) fold_elems<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, e, 1, out, nullptr);
+}
+
 // ---------------------------------------------------------------------------
 // Pull kernels launched after a HOST-side hand-off (p2p / RMA: the producer's
 // kernel finished and the host saw it) read peer memory mapped through IPC.
@@ -643,6 +720,12 @@ __device__ __forceinline__ void pull_release(int on) {
 // Returns false (and sets *err) if a peer did not arrive within the timeout.
 // ---------------------------------------------------------------------------
 constexpr int kSigShift = 25;
+
+// Phase timestamp k of this block (mpigx_comm_set_stamps, diagnostic): one
+// lane stores the 100 MHz device wall clock; a scalar branch when off.
+__device__ __forceinline__ void stamp(const PeerView& pv, int k) {
+  if (pv.stamps && threadIdx.x == 0) pv.stamps[(size_t)blockIdx.x * 8 + k] = wall_clock64();
+}
 
 __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, int* abort = nullptr,
                                              unsigned key = 0, bool check_key = false) {

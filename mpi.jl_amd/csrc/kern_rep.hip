@@ -93,11 +93,66 @@ hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs
   }
   return hipGetLastError();
 }
+
+// ar_zc_kernel instantiations (kernels.hpp): NMAX = n rounded up to a power
+// of two, U = 16 / NMAX; SH_FULL when every one of the NMAX leaves is present
+// with no pre-step, else SH_PRE.  nmax/shape come from arzc_shape (launch.hpp).
+template <class OP>
+hipError_t arzc_op(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a) {
+  if (nmax == 2)
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 2, SH_FULL, 8>), grid, dim3(kThreads), 0, s, a);
+  else if (nmax == 4 && shape == SH_FULL)
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_FULL, 4>), grid, dim3(kThreads), 0, s, a);
+  else if (nmax == 4)
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_PRE, 4>), grid, dim3(kThreads), 0, s, a);
+  else if (shape == SH_FULL)
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_FULL, 2>), grid, dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_PRE, 2>), grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+// Resident 256-thread blocks per CU of the kernels that spin on their peers
+// (fold / ring / scan / ar_zc) for an nmax (8: n <= 8, 16: n <= 16): the
+// smallest over the instantiations a communicator of that size can launch.
+template <class K>
+int occ1(K k) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return nb;
+}
+template <class OP>
+int occ_op(int nmax) {
+  int m = 1 << 20;
+  auto lo = [&](int v) { m = v < m ? v : m; };
+  if (nmax <= 8) {
+    lo(occ1(fold_kernel<OP, T, 8, S_TREE>));
+    lo(occ1(fold_kernel<OP, T, 8, S_LINEAR>));
+    lo(occ1(ar_zc_kernel<OP, T, 2, SH_FULL, 8>));
+    lo(occ1(ar_zc_kernel<OP, T, 4, SH_FULL, 4>));
+    lo(occ1(ar_zc_kernel<OP, T, 4, SH_PRE, 4>));
+    lo(occ1(ar_zc_kernel<OP, T, 8, SH_FULL, 2>));
+    lo(occ1(ar_zc_kernel<OP, T, 8, SH_PRE, 2>));
+  } else {
+    lo(occ1(fold_kernel<OP, T, 16, S_TREE>));
+    lo(occ1(fold_kernel<OP, T, 16, S_LINEAR>));
+  }
+  lo(occ1(ring_kernel<OP, T>));
+  lo(occ1(scan_kernel<OP, T>));
+  return m;
+}
 }  // namespace
 
 // Per-op entry points: declared for every op code here (the dispatchers of
 // part 6 reference only the valid ones), defined by the part that owns the op.
+#define MPIGX_ARZC_FN(K) MPIGX_CAT4(launch_arzc_, MPIGX_REP_NAME, _o, K)
+#define MPIGX_OCC_FN(K) MPIGX_CAT4(occupancy_, MPIGX_REP_NAME, _o, K)
 #define MPIGX_DECL_OP(K)                                                                               \
+  hipError_t MPIGX_ARZC_FN(K)(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a);      \
+  int MPIGX_OCC_FN(K)(int nmax);                                                                       \
   hipError_t MPIGX_FOLD_FN(K)(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a);      \
   hipError_t MPIGX_RING_FN(K)(dim3 grid, hipStream_t s, const RingArgs& a);                            \
   hipError_t MPIGX_SCAN_FN(K)(dim3 grid, hipStream_t s, const ScanArgs& a);                            \
@@ -111,6 +166,14 @@ MPIGX_DECL_OP(6) MPIGX_DECL_OP(7) MPIGX_DECL_OP(8) MPIGX_DECL_OP(9) MPIGX_DECL_O
   hipError_t MPIGX_FOLD_FN(K)(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a) {     \
     if constexpr (valid_op(K)) return fold_op<OpOf<K>::type>(nmax, sched, grid, s, a);                 \
     return hipErrorInvalidValue;                                                                       \
+  }                                                                                                    \
+  hipError_t MPIGX_ARZC_FN(K)(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a) {     \
+    if constexpr (valid_op(K)) return arzc_op<OpOf<K>::type>(nmax, shape, grid, s, a);                 \
+    return hipErrorInvalidValue;                                                                       \
+  }                                                                                                    \
+  int MPIGX_OCC_FN(K)(int nmax) {                                                                      \
+    if constexpr (valid_op(K)) return occ_op<OpOf<K>::type>(nmax);                                     \
+    return 1 << 20;                                                                                    \
   }                                                                                                    \
   hipError_t MPIGX_RING_FN(K)(dim3 grid, hipStream_t s, const RingArgs& a) {                           \
     if constexpr (valid_op(K)) {                                                                       \
@@ -189,6 +252,29 @@ hipError_t MPIGX_ACC_FN(17)(dim3 grid, hipStream_t s, const AccArgs& a) {
 hipError_t MPIGX_CAT(launch_fold_, MPIGX_REP_NAME)(int op, int nmax, int sched, dim3 grid, hipStream_t s,
                                                   const FoldArgs& a) {
   MPIGX_SWITCH(MPIGX_FOLD_FN, nmax, sched, grid, s, a)
+}
+hipError_t MPIGX_CAT(launch_arzc_, MPIGX_REP_NAME)(int op, int nmax, int shape, dim3 grid, hipStream_t s,
+                                                  const FoldArgs& a) {
+  MPIGX_SWITCH(MPIGX_ARZC_FN, nmax, shape, grid, s, a)
+}
+int MPIGX_CAT(occupancy_, MPIGX_REP_NAME)(int nmax) {
+  int m = 1 << 20;
+  auto lo = [&](int v) { m = v < m ? v : m; };
+  lo(MPIGX_OCC_FN(0)(nmax));
+  lo(MPIGX_OCC_FN(1)(nmax));
+  if constexpr (!kCplx) {
+    lo(MPIGX_OCC_FN(2)(nmax));
+    lo(MPIGX_OCC_FN(3)(nmax));
+    lo(MPIGX_OCC_FN(4)(nmax));
+    lo(MPIGX_OCC_FN(5)(nmax));
+    lo(MPIGX_OCC_FN(6)(nmax));
+  }
+  if constexpr (kInt) {
+    lo(MPIGX_OCC_FN(7)(nmax));
+    lo(MPIGX_OCC_FN(8)(nmax));
+    lo(MPIGX_OCC_FN(9)(nmax));
+  }
+  return m;
 }
 hipError_t MPIGX_CAT(launch_ring_, MPIGX_REP_NAME)(int op, dim3 grid, hipStream_t s, const RingArgs& a) {
   MPIGX_SWITCH(MPIGX_RING_FN, grid, s, a)

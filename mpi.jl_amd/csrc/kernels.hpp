@@ -153,7 +153,9 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     // (skipped everywhere if any rank's view of the mappings is stale)
     const int n = pv.n, r = pv.rank;
     int ab;
+    stamp(pv, 0);
     if (!zc_enter(pv, ep++, &ab)) return 0;  // every rank's send buffer is ready
+    stamp(pv, 1);
     if (!ab) {
     const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
     const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
@@ -166,7 +168,9 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
     fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
     }
+    stamp(pv, 2);
     if (!rank_barrier(pv, ep++, &ab)) return 0;  // every reduced chunk is in its owner's recvbuf
+    stamp(pv, 3);
     if (!ab) {
     char* dsts[NMAX];
     const char* srcs[NMAX];
@@ -187,7 +191,9 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     }
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
     }
+    stamp(pv, 4);
     rank_barrier(pv, ep++, &ab);  // nobody reads my buffers any more
+    stamp(pv, 5);
     return ab;
   }
 
@@ -251,6 +257,8 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     char* dsts[NMAX];
     const char* srcs[NMAX];
     long long lens[NMAX];
+    stamp(pv, 0);
+    stamp(pv, 1);
     // phase 1: slice b of my chunk p -> rank p's slot [r], all peers at once
 #pragma unroll
     for (int j = 0; j < NMAX; ++j) {
@@ -267,10 +275,12 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       }
     }
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    stamp(pv, 2);
     // phase 2 writes into the peers' recvbufs through the view's mappings:
     // the barrier checks every rank uses the same view (zc_enter)
     int ab = pv.zc_bad;
     if (!rank_barrier(pv, ep++, &ab, pv.zc_key, true)) return 0;
+    stamp(pv, 3);
     if (!ab) {
     // phase 2: fold my chunk (slots = local HBM) into my recvbuf, then write
     // the reduced slice into every peer's recvbuf
@@ -299,7 +309,9 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     }
     block_gather<NMAX>(dsts, srcs, lens, n - 1);
     }
+    stamp(pv, 4);
     rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
+    stamp(pv, 5);
     return ab;
   }
 
@@ -449,6 +461,95 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
   }
   rank_barrier(pv, ep++);
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Zero-copy two-shot Allreduce (M_AR_ZC, the headline path >= MPIGX_ZC_MIN,
+// MPICH tree schedule, n <= 8) in a kernel of its own, sized by the rank
+// count.  The all-modes fold_kernel keeps ONE vector's leaves in flight per
+// thread (n loads; 2 at n = 2) and gathers one vector per peer (1 load at
+// n = 2): one 256-block grid then holds ~16 KB of loads in flight per CU,
+// a third of what HBM needs (the n = 2 same-device two-shot ran at 0.46 of
+// HBM against 0.79 for the local fold).  Here NMAX = n rounded
+// up to a power of two (2, 4, 8) is a compile-time constant, and U = 16 /
+// NMAX vectors per thread per iteration keep ~16 loads outstanding in both
+// phases at every n:
+//   entry barrier (zero-copy view check) -> RS: fold slice b of my chunk r
+//   from every rank's sendbuf into my recvbuf -> barrier -> AG: slice b of
+//   chunk p from rank p's recvbuf, every peer interleaved -> exit barrier.
+// Same chunk / slice partition, barriers and fold schedule as fold_body's
+// M_AR_ZC (identical bits; that path still serves LINEAR order and n > 8).
+// SHAPE: SH_FULL (n = NMAX, no pre-step: every leaf present, no guards) or
+// SH_PRE (pre-step partners and / or fewer leaves, guarded).
+// ---------------------------------------------------------------------------
+template <class OP, class T, int NMAX, int SHAPE, int U>
+__global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
+  __shared__ FoldArgs A;  // indexed by runtime ranks below (see fold_kernel)
+  {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&A0);
+    uint32_t* d = reinterpret_cast<uint32_t*>(&A);
+    for (unsigned i = threadIdx.x; i < sizeof(FoldArgs) / 4; i += blockDim.x) d[i] = w[i];
+    __syncthreads();
+  }
+  const PeerView& pv = A.pv;
+  const T* const* src = reinterpret_cast<const T* const*>(A.src);
+  const T* const* src2 = reinterpret_cast<const T* const*>(A.src2);
+  T* recv = (T*)A.recv;
+  const int n = pv.n, r = pv.rank, b = blockIdx.x, es = A.esize;
+  const long long tid = threadIdx.x, nt = blockDim.x;
+  uint64_t ep = pv.epoch;
+  int ab;
+  stamp(pv, 0);
+  if (!zc_enter(pv, ep++, &ab)) {
+    signal_done(pv, 0);
+    return;
+  }
+  stamp(pv, 1);
+  if (!ab) {
+    const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+    bool vec = ((uintptr_t)recv & 15) == 0;
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s)
+      if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
+    if constexpr (SHAPE == SH_PRE) {
+#pragma unroll
+      for (int s = 0; s < NMAX / 2; ++s)
+        if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
+    }
+    if (vec) fold_span<OP, T, NMAX, SHAPE, U>(A, src, src2, lo, hi, recv);
+    else fold_range<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, lo, hi, recv, nullptr, false, tid, nt);
+  }
+  stamp(pv, 2);
+  if (!rank_barrier(pv, ep++, &ab)) {  // every reduced chunk is in its owner's recvbuf
+    signal_done(pv, 0);
+    return;
+  }
+  stamp(pv, 3);
+  if (!ab) {
+    char* dsts[NMAX];
+    const char* srcs[NMAX];
+    long long lens[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      dsts[j] = nullptr;
+      srcs[j] = nullptr;
+      lens[j] = 0;
+      if (j + 1 < n) {
+        const int p = (r + 1 + j) % n;
+        const long long d0 = lmin((long long)p * A.chunk, A.count), d1 = lmin(d0 + A.chunk, A.count);
+        const long long l2 = lmin(d0 + (long long)b * A.slice, d1), h2 = lmin(l2 + A.slice, d1);
+        dsts[j] = (char*)(recv + l2);
+        srcs[j] = A.zc_recv[p] + l2 * es;
+        lens[j] = (h2 - l2) * es;
+      }
+    }
+    block_gather_u<NMAX, U>(dsts, srcs, lens, n - 1);
+  }
+  stamp(pv, 4);
+  rank_barrier(pv, ep++, &ab);  // nobody reads my buffers any more
+  stamp(pv, 5);
+  signal_done(pv, ab);
 }
 
 // ---------------------------------------------------------------------------

@@ -13,7 +13,23 @@ using AccLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const AccAr
 using ScanLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const ScanArgs& a);
 using RingLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const RingArgs& a);
 
+using ArzcLauncher = hipError_t (*)(int op, int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a);
+using OccQuery = int (*)(int nmax);
+
+// ar_zc_kernel (kernels.hpp) instantiation for a communicator of n <= 8
+// ranks and the planned fold (ntree leaves, rem pre-step pairs): NMAX = n
+// rounded up to a power of two, SH_FULL when all NMAX leaves are present
+// without a pre-step.  Returns false when the kernel does not apply (n > 8).
+inline bool arzc_shape(int n, int ntree, int rem, int* nmax, int* shape) {
+  if (n < 2 || n > 8) return false;
+  *nmax = n <= 2 ? 2 : n <= 4 ? 4 : 8;
+  *shape = (rem == 0 && ntree == *nmax) ? SH_FULL : SH_PRE;
+  return true;
+}
+
 #define MPIGX_DECL_REP(NAME)                                                                     \
+  hipError_t launch_arzc_##NAME(int op, int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a); \
+  int occupancy_##NAME(int nmax); \
   hipError_t launch_fold_##NAME(int op, int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a); \
   hipError_t launch_scan_##NAME(int op, dim3 grid, hipStream_t s, const ScanArgs& a); \
   hipError_t launch_ring_##NAME(int op, dim3 grid, hipStream_t s, const RingArgs& a); \
@@ -25,6 +41,7 @@ MPIGX_DECL_REP(bf16)
 #undef MPIGX_DECL_REP
 
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a);
+int occupancy_copy(int nmax);
 hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a);
 hipError_t launch_xfer(hipStream_t s, const XferArgs& a);
 hipError_t launch_pack(hipStream_t s, const PackArgs& a);

@@ -142,6 +142,42 @@ RingLauncher ring_launcher(Rep r) {
     default: return nullptr;
   }
 }
+ArzcLauncher arzc_launcher(Rep r) {
+  switch (r) {
+    case R_I8: return launch_arzc_i8;
+    case R_U8: return launch_arzc_u8;
+    case R_I16: return launch_arzc_i16;
+    case R_U16: return launch_arzc_u16;
+    case R_I32: return launch_arzc_i32;
+    case R_U32: return launch_arzc_u32;
+    case R_I64: return launch_arzc_i64;
+    case R_U64: return launch_arzc_u64;
+    case R_F32: return launch_arzc_f32;
+    case R_F64: return launch_arzc_f64;
+    case R_C64: return launch_arzc_c64;
+    case R_C128: return launch_arzc_c128;
+    case R_BF16: return launch_arzc_bf16;
+    default: return nullptr;
+  }
+}
+// Resident 256-thread blocks per CU of every kernel that spins on its peers
+// (all types and ops, the instantiations of this nmax): the grid cap's
+// occupancy (comm_init).  Queried once per process and nmax.
+int spin_occupancy(int nmax) {
+  static int cached[2] = {-1, -1};
+  int& v = cached[nmax > 8 ? 1 : 0];
+  if (v >= 0) return v;
+  const OccQuery qs[] = {occupancy_i8,  occupancy_u8,  occupancy_i16, occupancy_u16, occupancy_i32,
+                         occupancy_u32, occupancy_i64, occupancy_u64, occupancy_f32, occupancy_f64,
+                         occupancy_c64, occupancy_c128, occupancy_bf16};
+  int m = occupancy_copy(nmax);
+  for (OccQuery q : qs) {
+    const int o = q(nmax);
+    m = o < m ? o : m;
+  }
+  v = m;
+  return v;
+}
 ScanLauncher scan_launcher(Rep r) {
   switch (r) {
     case R_I8: return launch_scan_i8;
@@ -224,6 +260,7 @@ PeerView make_view(mpigx_comm* c) {
   pv.dcount = c->dcount_dev;
   pv.dbase = c->dcount_total;
   pv.seq = c->launch_seq + 1;
+  pv.stamps = c->stamps;
   for (int p = 0; p < c->n; ++p) {
     pv.sig[p] = c->peer_sig[p];
     pv.stage[p] = c->peer_stage[p];
@@ -245,6 +282,8 @@ void note_launch(mpigx_comm* c, const PeerView& pv, unsigned grid) {
     c->unflagged = true;
   }
 }
+
+int barrier_launch(mpigx_comm* c);
 
 // After enqueueing: in blocking mode wait and translate device errors.  The
 // wait spins on the host-mapped completion counter (every block of every
@@ -296,8 +335,12 @@ int grid_for(mpigx_comm* c, long long bytes) {
 // Fold schedule for an n-leaf reduction (MPICH single-node semantics):
 //   small (count*size <= 2048 or count < pof2): binomial tree over relative
 //   ranks (rel = (rank - root) mod n), lower subtree = inout;
-//   large: Rabenseifner — odd rank 2i+1 folds 2i (pre-step, inout = odd),
-//   then the pairwise tree over newranks with owner-based operand roles.
+//   large: Rabenseifner as MPICH's Reduce runs it (reduce_scatter_gather;
+//   one node's Allreduce = Reduce to rank 0 + Bcast) — even rank 2i folds
+//   odd rank 2i+1 (pre-step, inout = even), then the pairwise tree over
+//   newranks with owner-based operand roles.  The pre-step roles matter for
+//   MIN/MAX with NaN / +-0 only; the large-count MPICH fixtures pin them
+//   (tests/golden/mpich_large.npz, n = 5: an odd-inout pre-step differs).
 // `ptrs[k]` is what leaf k reads for rank k (staging base or user pointer).
 void plan_schedule(mpigx_comm* c, FoldArgs& a, int n, int root, long long count_total, int esize,
                    const void* const* ptrs, int* nmax, int* sched, int order) {
@@ -326,8 +369,8 @@ void plan_schedule(mpigx_comm* c, FoldArgs& a, int n, int root, long long count_
     a.rem = rem;
     for (int s = 0; s < pof2; ++s) {
       if (s < rem) {
-        a.src[s] = ptrs[2 * s + 1];
-        a.src2[s] = ptrs[2 * s];
+        a.src[s] = ptrs[2 * s];       // inout
+        a.src2[s] = ptrs[2 * s + 1];  // in
       } else {
         a.src[s] = ptrs[s + rem];
       }
@@ -392,6 +435,10 @@ char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemH
       return im.base;
     }
   void* ptr = nullptr;
+  if (c->test_import_fail > 0) {  // fault injection (MPIGX_TEST_IMPORT_FAIL, tests only)
+    --c->test_import_fail;
+    return nullptr;
+  }
   if (hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
@@ -508,9 +555,11 @@ void zc_optimistic(mpigx_comm* c, const void* send, void* recv, ZcLaunch* z) {
 }
 
 // Exchange: every rank's registration, imports, a new view.  Returns 1 =
-// launch with *z (z->bad = 1 if an import failed here: the launch aborts on
-// every rank and reports MPI_ERR_INTERN), 0 = some rank's buffer is not
-// exportable (every rank takes the staged path), < 0 = -error.
+// launch with *z, 0 = some rank's buffer is not exportable or some rank could
+// not import a peer's (every rank takes the staged path: a second 4-byte
+// exchange agrees on the import results, so no rank launches a zero-copy
+// kernel that a peer aborts — in stream-ordered mode nobody would learn of
+// that abort and recvbuf would stay unwritten), < 0 = -error.
 int zc_exchange(mpigx_comm* c, const void* send, void* recv, ZcLaunch* z) {
   memset(z, 0, sizeof *z);
   const int n = c->n;
@@ -543,11 +592,11 @@ int zc_exchange(mpigx_comm* c, const void* send, void* recv, ZcLaunch* z) {
     v.ps[q] = sb + all[q].off[0];
     v.pr[q] = rb + all[q].off[1];
   }
-  if (!ok) {
-    z->bad = 1;
-    z->key = id;
-    return 1;
-  }
+  int iok = ok ? 1 : 0, iall[kMaxRanks];
+  const int rc2 = host_allgather(c, &iok, sizeof iok, iall);
+  if (rc2) return -rc2;
+  for (int q = 0; q < n; ++q)
+    if (!iall[q]) return 0;
   v.tick = ++c->tick;
   if (c->zviews.size() >= kZcViews) {
     size_t old = 0;
@@ -598,8 +647,9 @@ int zc_run(mpigx_comm* c, const void* send, void* recv, bool* staged, F&& launch
   }
   int rc = launch(z);
   if (!rc) rc = finish(c);
-  if (!rc && zc_take_stale(c)) rc = MPIGX_ERR_INTERN;  // an import failed on some rank
-  if (!rc && z.bad) rc = MPIGX_ERR_INTERN;             // ... here (stream-ordered: known locally)
+  // every rank imported every mapping (agreed above), so an abort here means
+  // a broken protocol, not a missing mapping
+  if (!rc && zc_take_stale(c)) rc = MPIGX_ERR_INTERN;
   return rc;
 }
 
@@ -631,7 +681,13 @@ int allreduce_zc(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeIn
   a.chunk = rup(cdiv(count, n), vec);
   const int grid = grid_for(c, a.chunk * es);
   a.slice = rup(cdiv(a.chunk, grid), vec);
-  HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
+  // the dedicated kernel (kernels.hpp ar_zc_kernel) for the MPICH tree at
+  // n <= 8; the all-modes fold_kernel for LINEAR order and n > 8 (same bits)
+  int znmax, zshape;
+  if (sched == S_TREE && c->algo != MPIGX_ALGO_PULL_GENERIC && arzc_shape(n, a.ntree, a.rem, &znmax, &zshape))
+    HIPCK(arzc_launcher(t->rep)(oc, znmax, zshape, dim3(grid), c->stream, a));
+  else
+    HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
   note_launch(c, a.pv, grid);
   c->epoch += 3;
   return MPIGX_SUCCESS;
@@ -652,13 +708,8 @@ int allreduce_push(mpigx_comm* c, const ZcLaunch& z, const void* send, long long
     // their previous launch having ended with one; an LL launch does not (a
     // peer may still be unpacking into its arena), so barrier first.  The
     // flag follows the same collective sequence on every rank.
-    CopyArgs b;
-    memset(&b, 0, sizeof b);
-    b.pv = make_view(c);
-    b.mode = C_BARRIER;
-    HIPCK(launch_copy(dim3(1), c->stream, b));
-    note_launch(c, b.pv, 1);
-    c->epoch += 1;
+    const int rc = barrier_launch(c);
+    if (rc) return rc;
     c->ll_unfenced = false;
   }
   for (long long off = 0; off < count; off += round) {
@@ -723,8 +774,7 @@ int ring_strides(int n, int want, int* st) {
 int allreduce_ring(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeInfo* t, int oc) {
   const int n = c->n, r = c->rank, es = t->size;
   const int vec = es >= 16 ? 1 : 16 / es;
-  int want = (int)env_ll("MPIGX_RING_CHANNELS", 1);
-  want = want < 1 ? 1 : want > kMaxRings ? kMaxRings : want;
+  const int want = c->ring_channels;  // 1..kMaxRings (knob)
   int st[kMaxRings];
   const int nch = ring_strides(n, want, st);
   RingLauncher L = ring_launcher(t->rep);
@@ -764,13 +814,12 @@ int allreduce_ring(mpigx_comm* c, const ZcLaunch& z, long long count, const Type
 // LL exchange (device.hpp ll_exchange) for a `bytes`-byte message: taken by
 // small Allreduce / Reduce / Scan / Exscan unless MPIGX_ALGO forces the
 // staged one-/two-shot.  The decision is identical on every rank (same count,
-// thresholds that init checked to agree, same environment).
+// knobs that init checked to agree and that only change collectively).
 // MPIGX_ALGO=ll takes it up to the area's capacity (MPIGX_LL_MAX), otherwise
 // up to MPIGX_LL_AUTO.
 bool ll_fits(mpigx_comm* c, long long bytes) {
-  const char* algo = getenv("MPIGX_ALGO");
-  if (algo && (!strcmp(algo, "oneshot") || !strcmp(algo, "twoshot"))) return false;
-  const bool forced = algo && !strcmp(algo, "ll");
+  if (c->algo == MPIGX_ALGO_ONESHOT || c->algo == MPIGX_ALGO_TWOSHOT) return false;
+  const bool forced = c->algo == MPIGX_ALGO_LL;
   return c->ll && bytes <= (forced ? c->ll_max : c->ll_auto);
 }
 bool ll_take(mpigx_comm* c, long long bytes) {
@@ -779,12 +828,45 @@ bool ll_take(mpigx_comm* c, long long bytes) {
 // This launch's LL pointers: push[p] = rank p's area (parity) at my sender
 // slot, *in = my own area (parity), and a flag no earlier launch of the same
 // parity used (the epoch is monotone and equal on every rank).
-void ll_fill(mpigx_comm* c, char** push, const char** in, long long* stride, unsigned* flag) {
+// The flag carries the epoch's low 31 bits; when the epoch enters a new
+// 2^31 generation (epoch >> 31 changes, on every rank at the same call) a
+// line last written exactly one generation earlier could carry the current
+// flag, so the area is cleared first: barrier (no rank still reads or writes
+// LL lines of earlier launches), every rank zeroes its own area, barrier (no
+// rank pushes before every area is clear); a zero line never matches a flag
+// (top bit set).  `pv` (the launch's view, made before this call) is renewed
+// after those launches.
+int barrier_launch(mpigx_comm* c);
+int ll_fill(mpigx_comm* c, PeerView& pv, char** push, const char** in, long long* stride, unsigned* flag) {
+  if ((unsigned)(c->epoch >> 31) != c->ll_gen) {
+    int rc = barrier_launch(c);
+    if (rc) return rc;
+    HIPCK(hipMemsetAsync(c->ll, 0, (size_t)2 * kMaxRanks * c->ll_stride, c->stream));
+    if ((rc = barrier_launch(c))) return rc;
+    c->ll_gen = (unsigned)(c->epoch >> 31);
+    const unsigned key = pv.zc_key;
+    const int bad = pv.zc_bad;
+    pv = make_view(c);
+    pv.zc_key = key;
+    pv.zc_bad = bad;
+  }
   const long long par = (long long)(c->ll_seq & 1) * kMaxRanks * c->ll_stride;
   for (int p = 0; p < c->n; ++p) push[p] = c->peer_ll[p] + par + (long long)c->rank * c->ll_stride;
   *in = c->ll + par;
   *stride = c->ll_stride;
   *flag = (unsigned)(c->epoch & 0x7fffffffu) | 0x80000000u;
+  return MPIGX_SUCCESS;
+}
+// one cross-rank barrier launch (copy_kernel C_BARRIER, one block)
+int barrier_launch(mpigx_comm* c) {
+  CopyArgs b;
+  memset(&b, 0, sizeof b);
+  b.pv = make_view(c);
+  b.mode = C_BARRIER;
+  HIPCK(launch_copy(dim3(1), c->stream, b));
+  note_launch(c, b.pv, 1);
+  c->epoch += 1;
+  return MPIGX_SUCCESS;
 }
 void ll_launched(mpigx_comm* c) {
   c->epoch += 1;
@@ -938,16 +1020,15 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   // elements per round: staging holds a whole round
   long long round = (long long)(c->stage_bytes / es);
   round = (round / (n * (long long)vec)) * n * vec;
-  const char* algo_env = getenv("MPIGX_ALGO");
+  const int algo = c->algo;  // knob: identical on every rank
   // count and the thresholds are identical on every rank, so is this test
-  if (all && n > 1 && c->zc_min > 0 && count * es >= c->zc_min &&
-      !(algo_env && !strcmp(algo_env, "oneshot"))) {
-    bool push = algo_env && !strcmp(algo_env, "push");
-    const bool ring = algo_env && !strcmp(algo_env, "ring");
+  if (all && n > 1 && c->zc_min > 0 && count * es >= c->zc_min && algo != MPIGX_ALGO_ONESHOT) {
+    bool push = algo == MPIGX_ALGO_PUSH;
+    const bool ring = algo == MPIGX_ALGO_RING;
     // no MPIGX_ALGO: the pull or the push two-shot, whichever measured faster
     // on this communicator (ar_tune_*); undecided, call 2 times the pull and
     // call 3 the push (call 1 registers the buffers)
-    const int timed = algo_env ? -1 : ar_tune_pick(c, &push);
+    const int timed = algo != MPIGX_ALGO_AUTO ? -1 : ar_tune_pick(c, &push);
     bool staged;
     const int rc = zc_run(c, send, recv, &staged, [&](const ZcLaunch& z) {
       if (ring) return allreduce_ring(c, z, count, t, oc);
@@ -999,8 +1080,8 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   }
   // below the zero-copy size: the measured variant for Allreduce (mt_*)
   int timed = -1, cls = -1;
-  int force = (all && !algo_env) ? mt_pick(c, TK_ALLREDUCE, count * es, &timed, &cls) : -1;
-  if (all && algo_env && !strcmp(algo_env, "ll2")) force = V_LL2;
+  int force = (all && algo == MPIGX_ALGO_AUTO) ? mt_pick(c, TK_ALLREDUCE, count * es, &timed, &cls) : -1;
+  if (all && algo == MPIGX_ALGO_LL2) force = V_LL2;
   if (force == V_LL2 && !ll2_fits(c, count * es, es)) force = -1;
   if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
   if (force == V_LL2) {
@@ -1015,7 +1096,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     a.count = count;
     a.send = send;
     a.recv = recv;
-    ll_fill(c, a.zc_recv, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    if (int e = ll_fill(c, a.pv, a.zc_recv, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
     a.slot_bytes = ustride;
     a.chunk = rup(cdiv(count, n), vec);
     const long long c0 = (long long)c->rank * a.chunk < count ? (long long)c->rank * a.chunk : count;
@@ -1044,7 +1125,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     a.root = root;
     a.send = send;
     a.recv = recv;
-    ll_fill(c, a.zc_recv, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    if (int e = ll_fill(c, a.pv, a.zc_recv, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
     a.slot_bytes = ustride;
     int nmax, sched;
     const void* ptrs[kMaxRanks];
@@ -1073,8 +1154,8 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     for (int p = 0; p < n; ++p) ptrs[p] = c->peer_stage[p];
     plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
     bool oneshot = cnt * es <= c->oneshot_max;
-    if (algo_env && !strcmp(algo_env, "oneshot")) oneshot = true;
-    if (algo_env && !strcmp(algo_env, "twoshot")) oneshot = false;
+    if (algo == MPIGX_ALGO_ONESHOT) oneshot = true;
+    if (algo == MPIGX_ALGO_TWOSHOT) oneshot = false;
     if (force == V_ONE || force == V_TWO) oneshot = force == V_ONE;
     int grid, nbar;
     if (oneshot) {
@@ -1363,6 +1444,167 @@ int mpigx_get_unique_id(mpigx_unique_id_t* id) {
 
 namespace {
 
+// ---- knobs (include/mpigx.h MPIGX_KNOB_*) ----------------------------------
+// Every path-selecting setting is read ONCE, here, per communicator; init
+// compares every rank's values (comm_init) and mpigx_comm_set_knob changes
+// them only collectively, so all ranks always take the same branch.
+const char* const kAlgoNames[] = {"", "ll", "ll2", "oneshot", "twoshot", "push", "ring", "pull", "pull_generic"};
+const char* const kKnobEnv[MPIGX_KNOB_COUNT] = {
+    "MPIGX_ALGO",   "MPIGX_BCAST",      "MPIGX_RING_CHANNELS", "MPIGX_MAX_BLOCKS",     "MPIGX_ONESHOT_MAX",
+    "MPIGX_ZC_MIN", "MPIGX_BCAST_SAG_MIN", "MPIGX_ZC_REQUIRE", "MPIGX_BYTES_PER_BLOCK", "MPIGX_LL_AUTO",
+    "MPIGX_AR_TUNE", "MPIGX_ZC_OPTIMISTIC", "MPIGX_SYNC_SPIN", "MPIGX_STAGING_BYTES",  "MPIGX_LL_MAX"};
+
+long long knob_value(const mpigx_comm* c, int k) {
+  switch (k) {
+    case MPIGX_KNOB_ALGO: return c->algo;
+    case MPIGX_KNOB_BCAST: return c->bcast_mode;
+    case MPIGX_KNOB_RING_CHANNELS: return c->ring_channels;
+    case MPIGX_KNOB_MAX_BLOCKS: return c->max_blocks;
+    case MPIGX_KNOB_ONESHOT_MAX: return c->oneshot_max;
+    case MPIGX_KNOB_ZC_MIN: return c->zc_min;
+    case MPIGX_KNOB_BCAST_SAG_MIN: return c->bcast_sag_min;
+    case MPIGX_KNOB_ZC_REQUIRE: return c->zc_require ? 1 : 0;
+    case MPIGX_KNOB_BYTES_PER_BLOCK: return c->bytes_per_block;
+    case MPIGX_KNOB_LL_AUTO: return c->ll_auto;
+    case MPIGX_KNOB_AR_TUNE: return c->ar_tune;
+    case MPIGX_KNOB_ZC_OPTIMISTIC: return c->zc_optimistic ? 1 : 0;
+    case MPIGX_KNOB_SYNC_SPIN: return c->sync_mode;
+    case MPIGX_KNOB_STAGING_BYTES: return (long long)c->stage_bytes;
+    case MPIGX_KNOB_LL_MAX: return c->ll_max;
+    default: return -1;
+  }
+}
+
+// Validates and applies one knob (init = true: the two allocation sizes may
+// be set too).  MPIGX_ERR_ARG for an unknown knob or an out-of-range value.
+int knob_apply(mpigx_comm* c, int k, long long v, bool init) {
+  auto in = [&](long long lo, long long hi) { return v >= lo && v <= hi; };
+  switch (k) {
+    case MPIGX_KNOB_ALGO:
+      if (!in(MPIGX_ALGO_AUTO, MPIGX_ALGO_PULL_GENERIC)) return MPIGX_ERR_ARG;
+      c->algo = (int)v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_BCAST:
+      if (!in(0, 2)) return MPIGX_ERR_ARG;
+      c->bcast_mode = (int)v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_RING_CHANNELS:
+      if (!in(1, kMaxRings)) return MPIGX_ERR_ARG;
+      c->ring_channels = (int)v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_MAX_BLOCKS: {
+      if (!in(1, kMaxBlocks)) return MPIGX_ERR_ARG;
+      c->max_blocks = (int)(v < c->max_blocks_cap ? v : c->max_blocks_cap);
+      return MPIGX_SUCCESS;
+    }
+    case MPIGX_KNOB_ONESHOT_MAX:
+      if (v < 0) return MPIGX_ERR_ARG;
+      c->oneshot_max = v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_ZC_MIN:
+      if (v < 0) return MPIGX_ERR_ARG;
+      c->zc_min = v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_BCAST_SAG_MIN:
+      if (v < 0) return MPIGX_ERR_ARG;
+      c->bcast_sag_min = v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_ZC_REQUIRE:
+      if (!in(0, 1)) return MPIGX_ERR_ARG;
+      c->zc_require = v != 0;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_BYTES_PER_BLOCK:
+      if (v < 16) return MPIGX_ERR_ARG;
+      c->bytes_per_block = v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_LL_AUTO:
+      if (v < 0) return MPIGX_ERR_ARG;
+      c->ll_auto = v < c->ll_max ? v : c->ll_max;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_AR_TUNE:
+      if (!in(0, 1)) return MPIGX_ERR_ARG;
+      if (v && !init && !c->ar_ev[0]) {  // the tuners' events (comm_init creates them when on)
+        HIPCK(hipEventCreate(&c->ar_ev[0]));
+        HIPCK(hipEventCreate(&c->ar_ev[1]));
+      }
+      c->ar_tune = (int)v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_ZC_OPTIMISTIC:
+      if (!in(0, 1)) return MPIGX_ERR_ARG;
+      c->zc_optimistic = v != 0;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_SYNC_SPIN:
+      if (!in(0, 1)) return MPIGX_ERR_ARG;
+      c->sync_mode = (int)v;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_STAGING_BYTES:
+      if (!init || v < 4096) return MPIGX_ERR_ARG;
+      c->stage_bytes = ((size_t)v + 4095) & ~(size_t)4095;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_LL_MAX:
+      if (!init) return MPIGX_ERR_ARG;
+      c->ll_max = v < 0 ? 0 : v > (4ll << 20) ? (4ll << 20) : v;
+      return MPIGX_SUCCESS;
+    default: return MPIGX_ERR_ARG;
+  }
+}
+
+// Defaults, then the environment.  Numeric knobs out of range are clamped as
+// before the knobs existed; an unknown MPIGX_ALGO / MPIGX_BCAST name fails
+// init (it used to be ignored silently on the rank that had it).
+int knobs_from_env(mpigx_comm* c) {
+  c->algo = MPIGX_ALGO_AUTO;
+  const char* a = getenv("MPIGX_ALGO");
+  if (a && *a) {
+    int v = -1;
+    for (int i = 1; i < (int)(sizeof kAlgoNames / sizeof kAlgoNames[0]); ++i)
+      if (!strcmp(a, kAlgoNames[i])) v = i;
+    if (v < 0) {
+      fprintf(stderr, "[mpigx] MPIGX_ALGO=%s: unknown algorithm\n", a);
+      return MPIGX_ERR_ARG;
+    }
+    c->algo = v;
+  }
+  c->bcast_mode = 0;
+  const char* bc = getenv("MPIGX_BCAST");
+  if (bc && *bc) {
+    if (!strcmp(bc, "direct")) c->bcast_mode = 1;
+    else if (!strcmp(bc, "sag")) c->bcast_mode = 2;
+    else {
+      fprintf(stderr, "[mpigx] MPIGX_BCAST=%s: expected direct or sag\n", bc);
+      return MPIGX_ERR_ARG;
+    }
+  }
+  long long rc_ = env_ll("MPIGX_RING_CHANNELS", 1);
+  c->ring_channels = (int)(rc_ < 1 ? 1 : rc_ > kMaxRings ? kMaxRings : rc_);
+  long long mb = env_ll("MPIGX_MAX_BLOCKS", 256);
+  c->max_blocks = (int)(mb < 1 ? 1 : mb > kMaxBlocks ? kMaxBlocks : mb);
+  c->oneshot_max = env_ll("MPIGX_ONESHOT_MAX", 256 << 10);
+  c->zc_min = env_ll("MPIGX_ZC_MIN", 16ll << 20);
+  c->bcast_sag_min = env_ll("MPIGX_BCAST_SAG_MIN", 256 << 10);
+  c->zc_require = env_ll("MPIGX_ZC_REQUIRE", 0) != 0;
+  // 8 KiB of message per block: 64 KiB one-shot drops 19.5 -> 6.7 us and
+  // 1 MiB two-shot 31 -> 19 us vs 64 KiB per block (tools/latency.py, 2 ranks)
+  c->bytes_per_block = env_ll("MPIGX_BYTES_PER_BLOCK", 8 << 10);
+  if (c->bytes_per_block < 16) c->bytes_per_block = 16;
+  c->stage_bytes = (size_t)env_ll("MPIGX_STAGING_BYTES", 512ll << 20);
+  c->stage_bytes = (c->stage_bytes + 4095) & ~(size_t)4095;
+  if (c->stage_bytes < 4096) c->stage_bytes = 4096;
+  c->ll_max = env_ll("MPIGX_LL_MAX", 256 << 10);
+  if (c->ll_max < 0) c->ll_max = 0;
+  if (c->ll_max > (4ll << 20)) c->ll_max = 4ll << 20;
+  // default LL range: 16 KiB — on ranks sharing one GPU the LL step beat the
+  // staged one-shot at 8 B but not at 64 KiB (profiles/r02_latency_*); the
+  // N>1 bench line measures both at 8 and 64 KiB (MPIGX_ALGO=ll forces LL)
+  c->ll_auto = env_ll("MPIGX_LL_AUTO", 16 << 10);
+  if (c->ll_auto > c->ll_max) c->ll_auto = c->ll_max;
+  if (c->ll_auto < 0) c->ll_auto = 0;
+  c->ar_tune = env_ll("MPIGX_AR_TUNE", 1) != 0 ? 1 : 0;
+  c->zc_optimistic = env_ll("MPIGX_ZC_OPTIMISTIC", 1) != 0;
+  c->sync_mode = env_ll("MPIGX_SYNC_SPIN", 1) != 0 ? 1 : 0;
+  return MPIGX_SUCCESS;
+}
+
 // Frees whatever a (possibly half-built) communicator holds: the device
 // allocations, the pinned page, peer mappings and the shm block.  Used by
 // mpigx_comm_free after its closing barrier and by every failed init.
@@ -1397,43 +1639,28 @@ void comm_release(mpigx_comm* c) {
 // caller it must unlink the shm name (rank 0 before every rank mapped it).
 int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   const int rank = c->rank, nranks = c->n, device = c->device;
-  c->max_blocks = (int)env_ll("MPIGX_MAX_BLOCKS", 256);
-  if (c->max_blocks < 1) c->max_blocks = 1;
-  if (c->max_blocks > kMaxBlocks) c->max_blocks = kMaxBlocks;
-  c->oneshot_max = env_ll("MPIGX_ONESHOT_MAX", 256 << 10);
-  c->zc_min = env_ll("MPIGX_ZC_MIN", 16ll << 20);
-  c->bcast_sag_min = env_ll("MPIGX_BCAST_SAG_MIN", 256 << 10);
-  c->zc_require = env_ll("MPIGX_ZC_REQUIRE", 0) != 0;
-  // 8 KiB of message per block: 64 KiB one-shot drops 19.5 -> 6.7 us and
-  // 1 MiB two-shot 31 -> 19 us vs 64 KiB per block (tools/latency.py, 2 ranks)
-  c->bytes_per_block = env_ll("MPIGX_BYTES_PER_BLOCK", 8 << 10);
-  c->stage_bytes = (size_t)env_ll("MPIGX_STAGING_BYTES", 512ll << 20);
-  c->stage_bytes = (c->stage_bytes + 4095) & ~(size_t)4095;
+  int krc = knobs_from_env(c);
+  if (krc) return krc;
   c->timeout_ticks = (uint64_t)(env_ll("MPIGX_TIMEOUT_MS", 60000) * 100000ll);  // 100 MHz clock
+  c->epoch = (uint64_t)env_ll("MPIGX_EPOCH_BASE", 1);  // test hook (LL flag generations); must agree
+  if (c->epoch < 1) c->epoch = 1;
+  c->ll_gen = (unsigned)(c->epoch >> 31);
+  c->test_import_fail = (int)env_ll("MPIGX_TEST_IMPORT_FAIL", 0);  // per rank: fault injection, not a knob
 
   HIPCK(hipMalloc(&c->stage, c->stage_bytes));
   const size_t sig_bytes = (size_t)kMaxBlocks * kMaxRanks * sizeof(uint64_t);
   HIPCK(hipExtMallocWithFlags((void**)&c->sig, sig_bytes, hipDeviceMallocUncached));
   HIPCK(hipMemset(c->sig, 0, sig_bytes));
-  // LL area for small Allreduce (M_AR_LL): uncached like the signal array, so
-  // peers' 64-bit line stores and my polls meet in HBM with no cache in between
-  c->ll_max = env_ll("MPIGX_LL_MAX", 256 << 10);
-  if (c->ll_max < 0) c->ll_max = 0;
-  if (c->ll_max > (4ll << 20)) c->ll_max = 4ll << 20;
+  // LL area for small messages (M_AR_LL ...): uncached like the signal array,
+  // so peers' 64-bit line stores and my polls meet in HBM with no cache in
+  // between
   c->ll_stride = rup(c->ll_max, 16) / 8 * kLLLine;
-  // default LL range: 16 KiB — on ranks sharing one GPU the LL step beat the
-  // staged one-shot at 8 B but not at 64 KiB (profiles/r02_latency_*); the
-  // N>1 bench line measures both at 8 and 64 KiB (MPIGX_ALGO=ll forces LL)
-  c->ll_auto = env_ll("MPIGX_LL_AUTO", 16 << 10);
-  // events of the large-Allreduce tuner (created here, so every rank has them
-  // or, with MPIGX_AR_TUNE=0 on every rank, none does)
-  c->ar_tune = (int)env_ll("MPIGX_AR_TUNE", 1);
+  // events of the measured algorithm choices (MPIGX_AR_TUNE)
   for (auto& x : c->mt_choice) x = -1;
   if (c->ar_tune) {
     HIPCK(hipEventCreate(&c->ar_ev[0]));
     HIPCK(hipEventCreate(&c->ar_ev[1]));
   }
-  if (c->ll_auto > c->ll_max) c->ll_auto = c->ll_max;
   if (c->ll_max > 0 && nranks > 1) {
     const size_t llb = (size_t)2 * kMaxRanks * c->ll_stride;
     HIPCK(hipExtMallocWithFlags((void**)&c->ll, llb, hipDeviceMallocUncached));
@@ -1444,8 +1671,6 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   HIPCK(hipHostGetDevicePointer((void**)&c->err_dev, c->err, 0));
   c->done = (volatile unsigned long long*)(c->err + 8);  // same pinned page, own 32-B slot
   HIPCK(hipHostGetDevicePointer((void**)&c->done_dev, (void*)c->done, 0));
-  c->zc_optimistic = env_ll("MPIGX_ZC_OPTIMISTIC", 1) != 0;
-  c->sync_mode = (int)env_ll("MPIGX_SYNC_SPIN", 1);
   HIPCK(hipMalloc((void**)&c->dcount_dev, 64));
   HIPCK(hipMemset(c->dcount_dev, 0, 64));
   HIPCK(hipDeviceSynchronize());
@@ -1501,6 +1726,11 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   HIPCK(hipGetDeviceProperties(&prop, device));
   me.pci_bus = prop.pciBusID;
   me.pci_dev = prop.pciDeviceID;
+  me.pci_domain = prop.pciDomainID;
+  me.cus = prop.multiProcessorCount;
+  me.occupancy = spin_occupancy(nranks <= 8 ? 8 : 16);
+  for (int k = 0; k < MPIGX_KNOB_COUNT; ++k) me.knobs[k] = knob_value(c, k);
+  me.epoch0 = c->epoch;
   me.stage_bytes = c->stage_bytes;
   me.stage_ptr = (unsigned long long)(uintptr_t)c->stage;
   me.sig_ptr = (unsigned long long)(uintptr_t)c->sig;
@@ -1514,12 +1744,54 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
     if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
     usleep(200);
   }
+  // every path-selecting knob must agree (a rank taking another branch than
+  // its peers would launch another kernel and spin until the device timeout)
+  for (int q = 0; q < nranks; ++q) {
+    const ShmRank& pr = c->shm->ranks[q];
+    for (int k = 0; k < MPIGX_KNOB_COUNT; ++k)
+      if (pr.knobs[k] != me.knobs[k]) {
+        fprintf(stderr, "[mpigx] rank %d: %s differs between ranks (%lld on rank %d, %lld on rank %d)\n", rank,
+                kKnobEnv[k], me.knobs[k], rank, pr.knobs[k], q);
+        return MPIGX_ERR_ARG;
+      }
+    if (pr.epoch0 != me.epoch0) return MPIGX_ERR_ARG;  // MPIGX_EPOCH_BASE likewise
+  }
+  // ranks sharing a device: every rank's grid of a spinning kernel must be
+  // resident at once (include/mpigx.h mpigx_comm_device_share)
+  {
+    int share = 1;
+    long long cap = kMaxBlocks;
+    for (int q = 0; q < nranks; ++q) {
+      const ShmRank& a = c->shm->ranks[q];
+      int k = 0;
+      for (int j = 0; j < nranks; ++j) {
+        const ShmRank& b = c->shm->ranks[j];
+        k += b.pci_domain == a.pci_domain && b.pci_bus == a.pci_bus && b.pci_dev == a.pci_dev;
+      }
+      share = k > share ? k : share;
+      // the occupancy API can admit one block per CU more than the hardware
+      // where SGPRs bind (>= 6 blocks of 256 threads, MI355X_MICROARCH.md
+      // "Residency"): one fewer there; VGPR-bound counts (<= 5) are exact
+      const long long occ = a.occupancy >= 6 ? a.occupancy - 1 : a.occupancy > 0 ? a.occupancy : 1;
+      const long long cq = (long long)a.cus * occ / k;
+      cap = cq < cap ? cq : cap;
+    }
+    c->dev_share = share;
+    c->max_blocks_cap = (int)(cap < 1 ? 1 : cap);
+    if (c->max_blocks > c->max_blocks_cap) c->max_blocks = c->max_blocks_cap;
+    const long long limit_share = env_ll("MPIGX_MAX_RANKS_PER_DEVICE", 10);
+    if (share > limit_share) {
+      fprintf(stderr,
+              "[mpigx] %d ranks share one GPU (limit MPIGX_MAX_RANKS_PER_DEVICE=%lld): more rank processes than "
+              "that did not all get hardware queues at once; bind ranks to distinct GPUs\n",
+              share, limit_share);
+      return MPIGX_ERR_OTHER;
+    }
+  }
   for (int q = 0; q < nranks; ++q) {
     if (q == rank) continue;
     const ShmRank& pr = c->shm->ranks[q];
-    if (pr.stage_bytes != c->stage_bytes) return MPIGX_ERR_ARG;  // MPIGX_STAGING_BYTES must agree
-    if (pr.ll_bytes != me.ll_bytes) return MPIGX_ERR_ARG;        // MPIGX_LL_MAX likewise
-    c->same_device[q] = pr.pci_bus == me.pci_bus && pr.pci_dev == me.pci_dev;
+    c->same_device[q] = pr.pci_domain == me.pci_domain && pr.pci_bus == me.pci_bus && pr.pci_dev == me.pci_dev;
     if (pr.pid == me.pid) {
       c->peer_stage[q] = (char*)(uintptr_t)pr.stage_ptr;
       c->peer_sig[q] = (uint64_t*)(uintptr_t)pr.sig_ptr;
@@ -1718,6 +1990,41 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t c, int order) {
   return MPIGX_SUCCESS;
 }
 
+// Collective: every rank's (knob, value) over the control plane; any
+// difference -> MPIGX_ERR_ARG everywhere and nothing changes.
+int mpigx_comm_set_knob(mpigx_comm_t c, int knob, long long value) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (c->broken) return MPIGX_ERR_OTHER;
+  struct {
+    long long knob, value;
+  } mine = {knob, value}, all[kMaxRanks];
+  if (c->n > 1) {
+    const int rc = host_allgather(c, &mine, sizeof mine, all);
+    if (rc) return rc;
+    for (int q = 0; q < c->n; ++q)
+      if (all[q].knob != mine.knob || all[q].value != mine.value) return MPIGX_ERR_ARG;
+  }
+  if (knob < 0 || knob >= MPIGX_KNOB_COUNT) return MPIGX_ERR_ARG;
+  return knob_apply(c, knob, value, false);
+}
+int mpigx_comm_get_knob(mpigx_comm_t c, int knob, long long* value) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (knob < 0 || knob >= MPIGX_KNOB_COUNT || !value) return MPIGX_ERR_ARG;
+  *value = knob_value(c, knob);
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_device_share(mpigx_comm_t c, int* ranks, int* cap) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (ranks) *ranks = c->dev_share;
+  if (cap) *cap = c->max_blocks_cap;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_set_stamps(mpigx_comm_t c, void* stamps) {
+  if (!c) return MPIGX_ERR_COMM;
+  c->stamps = (unsigned long long*)stamps;
+  return MPIGX_SUCCESS;
+}
+
 // ---------------------------------------------------------------------------
 int mpigx_barrier(mpigx_comm_t c) {
   int rc = check_comm(c);
@@ -1778,15 +2085,15 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
   // direct pull from the root (one barrier less) for small messages or two
   // ranks; scatter + allgather when the root's links would be the bottleneck.
   // The choice depends only on (bytes, n, env), identical on every rank.
-  const char* env = getenv("MPIGX_BCAST");
+  const bool env = c->bcast_mode != 0;  // MPIGX_BCAST knob: 1 direct, 2 sag
   bool sag = c->n >= 3 && bytes >= c->bcast_sag_min;
-  if (env && !strcmp(env, "direct")) sag = false;
-  if (env && !strcmp(env, "sag")) sag = c->n >= 2;
+  if (c->bcast_mode == 1) sag = false;
+  if (c->bcast_mode == 2) sag = c->n >= 2;
   // (zero-copy first when the size asks for it: tests force it at every size)
   // below the zero-copy size: LL or the staged copy, measured (mt_*)
   const bool zc_size = c->zc_min > 0 && bytes >= c->zc_min;
   int timed = -1, cls = -1;
-  const int force = (!env && !getenv("MPIGX_ALGO") && !zc_size) ? mt_pick(c, TK_BCAST, bytes, &timed, &cls) : -1;
+  const int force = (!env && c->algo == MPIGX_ALGO_AUTO && !zc_size) ? mt_pick(c, TK_BCAST, bytes, &timed, &cls) : -1;
   if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
   if (force >= 0 ? force == V_LL : (!env && copy_ll_take(c, bytes) && !zc_size)) {
     // small: the root's lines straight into every peer's LL area (C_BCAST_LL)
@@ -1798,7 +2105,7 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
     a.bytes = bytes;
     a.send = buf;
     a.recv = buf;
-    ll_fill(c, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    if (int e = ll_fill(c, a.pv, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
     const int g = grid_for(c, bytes);
     a.slice = rup(cdiv(bytes, g), 16);
     HIPCK(launch_copy(dim3(g), c->stream, a));
@@ -1889,7 +2196,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
   // below the zero-copy size: LL or the staged copy, measured (mt_*)
   const bool zc_size = c->zc_min > 0 && bytes * n >= c->zc_min && (!alltoall || !inplace);
   int timed = -1, cls = -1;
-  const int force = (!getenv("MPIGX_ALGO") && !zc_size)
+  const int force = (c->algo == MPIGX_ALGO_AUTO && !zc_size)
                         ? mt_pick(c, alltoall ? TK_ALLTOALL : TK_ALLGATHER, bytes, &timed, &cls) : -1;
   if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
   if (force >= 0 ? force == V_LL : (copy_ll_take(c, bytes) && !zc_size)) {
@@ -1902,7 +2209,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
     a.total = bytes;
     a.send = s;
     a.recv = recv;
-    ll_fill(c, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    if (int e = ll_fill(c, a.pv, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
     const int g = grid_for(c, bytes);
     a.slice = rup(cdiv(bytes, g), 16);
     HIPCK(launch_copy(dim3(g), c->stream, a));
@@ -2607,7 +2914,7 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
     a.recv = recvbuf;
     a.ll_ustride = rup(c->ll_max, 16);
     for (int p = 0; p < c->n; ++p) a.src[p] = c->stage + p * a.ll_ustride;
-    ll_fill(c, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag);
+    if (int e = ll_fill(c, a.pv, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
     HIPCK(L(oc, dim3(g), c->stream, a));
     note_launch(c, a.pv, g);
     ll_launched(c);

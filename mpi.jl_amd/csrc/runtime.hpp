@@ -15,13 +15,19 @@ namespace mpigx {
 // ---------------------------------------------------------------------------
 // shm block (one per communicator, mapped by every rank)
 // ---------------------------------------------------------------------------
-constexpr uint64_t kMagic = 0x6d70696778763032ull;  // "mpigxv02"
+constexpr uint64_t kMagic = 0x6d70696778763033ull;  // "mpigxv03"
 
 struct ShmRank {
   int pid;
   int device;
   int pci_bus;
   int pci_dev;
+  int pci_domain;
+  int occupancy;                 // resident blocks per CU of the spinning kernels (0: unknown)
+  int cus;                       // compute units of my device
+  int pad;
+  long long knobs[MPIGX_KNOB_COUNT];  // path-selecting settings read at init (must agree)
+  unsigned long long epoch0;          // first barrier epoch (MPIGX_EPOCH_BASE; must agree)
   unsigned long long stage_bytes;
   unsigned long long stage_ptr;  // raw pointer (same-process peers)
   unsigned long long sig_ptr;
@@ -218,11 +224,20 @@ struct mpigx_comm {
   // one-sided engine (created by the first window)
   mpigx::RmaState* rma = nullptr;
   bool in_progress = false;  // re-entrancy guard of rt::progress_all
-  // tuning
+  // tuning (the path-selecting knobs, include/mpigx.h MPIGX_KNOB_*: read once
+  // at init, checked to agree on every rank, changed only collectively)
   int max_blocks = 256;
+  int max_blocks_cap = mpigx::kMaxBlocks;  // residency cap (ranks sharing a device)
+  int dev_share = 1;                       // ranks on the most-loaded device
   long long oneshot_max = 256 << 10;
   long long bcast_sag_min = 256 << 10;  // Bcast: scatter+allgather from this size (n >= 3)
   long long bytes_per_block = 64 << 10;
+  int algo = MPIGX_ALGO_AUTO;           // MPIGX_ALGO
+  int bcast_mode = 0;                   // MPIGX_BCAST: 0 auto, 1 direct, 2 sag
+  int ring_channels = 1;                // MPIGX_RING_CHANNELS
+  unsigned long long* stamps = nullptr; // diagnostic phase timestamps (mpigx_comm_set_stamps)
+  unsigned ll_gen = 0;                  // LL flag generation (epoch >> 31) the LL area was cleared for
+  int test_import_fail = 0;             // MPIGX_TEST_IMPORT_FAIL: fail that many peer imports (tests)
   std::mutex mu;
 };
 

@@ -539,6 +539,48 @@ def set_reduce_order(comm: Comm, order: int):
     _check(lib().mpigx_comm_set_reduce_order(comm.val, order))
 
 
+# Path-selecting knobs (include/mpigx.h MPIGX_KNOB_*): read once per
+# communicator from the environment at init and checked to agree on every
+# rank; set_knob changes one collectively (every rank, same value).
+KNOBS = {"ALGO": 0, "BCAST": 1, "RING_CHANNELS": 2, "MAX_BLOCKS": 3, "ONESHOT_MAX": 4, "ZC_MIN": 5,
+         "BCAST_SAG_MIN": 6, "ZC_REQUIRE": 7, "BYTES_PER_BLOCK": 8, "LL_AUTO": 9, "AR_TUNE": 10,
+         "ZC_OPTIMISTIC": 11, "SYNC_SPIN": 12, "STAGING_BYTES": 13, "LL_MAX": 14}
+ALGOS = {None: 0, "": 0, "auto": 0, "ll": 1, "ll2": 2, "oneshot": 3, "twoshot": 4, "push": 5, "ring": 6,
+         "pull": 7, "pull_generic": 8}
+BCAST_MODES = {None: 0, "": 0, "auto": 0, "direct": 1, "sag": 2}
+
+
+def _knob_id(knob):
+    return KNOBS[knob.upper()] if isinstance(knob, str) else int(knob)
+
+
+def set_knob(comm: Comm, knob, value):
+    """mpigx extension, COLLECTIVE: every rank calls it with the same knob and
+    value (names as the MPIGX_* environment variables without the prefix;
+    ALGO / BCAST also take the environment's names, e.g. "ring", "sag", or
+    None for the default).  Differing values -> MPIError(MPI_ERR_ARG) on every
+    rank and nothing changes."""
+    k = _knob_id(knob)
+    if k == KNOBS["ALGO"] and (value is None or isinstance(value, str)):
+        value = ALGOS[value]
+    elif k == KNOBS["BCAST"] and (value is None or isinstance(value, str)):
+        value = BCAST_MODES[value]
+    _check(lib().mpigx_comm_set_knob(comm.val, k, int(value)))
+
+
+def get_knob(comm: Comm, knob) -> int:
+    v = ctypes.c_longlong(0)
+    _check(lib().mpigx_comm_get_knob(comm.val, _knob_id(knob), ctypes.byref(v)))
+    return v.value
+
+
+def device_share(comm: Comm):
+    """(ranks on the most-loaded GPU, grid cap of the spinning kernels)."""
+    r, cap = ctypes.c_int(0), ctypes.c_int(0)
+    _check(lib().mpigx_comm_device_share(comm.val, ctypes.byref(r), ctypes.byref(cap)))
+    return r.value, cap.value
+
+
 def _stream(comm):
     torch = _torch()
     s = torch.cuda.current_stream(comm.device).cuda_stream

@@ -210,15 +210,25 @@ def allreduce(inputs, dtname, opname, short_msg=2048):
     return [res.copy() for _ in range(n)]
 
 
-def _prestep(bufs, dtname, opname, n, pof2):
-    """Non-power-of-two pre-step: odd rank 2i+1 folds rank 2i: inout = odd."""
+def _prestep(bufs, dtname, opname, n, pof2, keep_even=False):
+    """Non-power-of-two pre-step between ranks 2i and 2i+1 (i < rem).
+    Allreduce (MPIR_Allreduce_intra_recursive_doubling /
+    _reduce_scatter_allgather): the even rank sends, the odd rank folds,
+    inout = odd, newrank i = rank 2i+1.  Reduce (MPIR_Reduce_intra_
+    reduce_scatter_gather, keep_even=True): the odd rank sends, the EVEN rank
+    folds, inout = even, newrank i = rank 2i.  The roles show only where
+    operands are ordered: MIN/MAX with NaN or +-0 (pinned by the large-count
+    MPICH fixtures, tests/golden/mpich_large.npz, n = 5)."""
     rem = n - pof2
     for i in range(rem):
-        bufs[2 * i + 1] = apply_op(opname, dtname, bufs[2 * i + 1], bufs[2 * i])
+        if keep_even:
+            bufs[2 * i] = apply_op(opname, dtname, bufs[2 * i], bufs[2 * i + 1])
+        else:
+            bufs[2 * i + 1] = apply_op(opname, dtname, bufs[2 * i + 1], bufs[2 * i])
     newrank = {}
     for r in range(n):
         if r < 2 * rem:
-            if r % 2:
+            if (r % 2 == 0) == keep_even:
                 newrank[r] = r // 2
         else:
             newrank[r] = r - rem
@@ -250,11 +260,15 @@ def _allreduce_rd(inputs, dtname, opname):
 
 
 def _allreduce_rsag(inputs, dtname, opname, out_ranks=None):
+    """Reduce-scatter + gather over newranks — the schedule of
+    MPIR_Reduce_intra_reduce_scatter_gather, which one node's Allreduce runs
+    (Reduce to rank 0 + Bcast, MPIR_Allreduce_intra_smp): pre-step with the
+    even rank as inout (_prestep keep_even)."""
     n = len(inputs)
     count = inputs[0].shape[0]
     pof2 = _pof2(n)
     bufs = [x.copy() for x in inputs]
-    rem, newrank, real = _prestep(bufs, dtname, opname, n, pof2)
+    rem, newrank, real = _prestep(bufs, dtname, opname, n, pof2, keep_even=True)
     cnts = [count // pof2] * (pof2 - 1) + [count - (count // pof2) * (pof2 - 1)]
     disps = [0]
     for i in range(1, pof2):

@@ -46,3 +46,40 @@ def make(dtname, opname, n, count, seed, edge=False):
 def valid_pairs(dtypes=None):
     names = dtypes or [d for d in M.DTYPES if M.DTYPES[d][2] != "none"]
     return [(d, o) for d in names for o in M.OPS if M.op_valid(d, o) == 0]
+
+
+# ---------------------------------------------------------------------------
+# splitmix64 inputs of the large-count MPICH fixtures (tests/golden/
+# gen_mpich_large.c gen(): same keying, same bit-to-value maps), regenerated
+# here so the fixture holds outputs only
+# ---------------------------------------------------------------------------
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64(x):
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def splitmix_input(kind, seed, rank, count, edge=False):
+    """Rank `rank`'s input of a large fixture case: kind "f32" / "f64" / "i64"."""
+    i = np.arange(count, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * np.uint64(0x100000001B3) ^ (np.uint64(rank) << np.uint64(40))
+    r = _splitmix64(base ^ i)
+    if kind == "i64":
+        return r.view(np.int64)
+    if kind == "f32":
+        v = ((r >> np.uint64(40)).astype(np.int64) - (1 << 23)).astype(np.float32) / np.float32(1 << 23)
+        tiny = np.float32(np.ldexp(np.float32(1), -149))
+        table = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, tiny, 1.0, -1.0], dtype=np.float32)
+    else:
+        v = ((r >> np.uint64(11)).astype(np.int64) - (1 << 52)).astype(np.float64) / 4503599627370496.0
+        table = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, np.ldexp(1.0, -1074), 1.0, -1.0])
+    if edge:
+        m = (r & np.uint64(15)) == 0
+        v[m] = table[((r[m] >> np.uint64(4)) & np.uint64(7)).astype(np.int64)]
+    return v

@@ -30,7 +30,9 @@ IN_PLACE = ctypes.c_void_p(-1 & ((1 << 64) - 1))
 # "ll": LL up to its capacity (MPIGX_LL_MAX), the default choice above it;
 # "ll2": the LL two-shot where a chunk fits half an LL slot;
 # "oneshot"/"twoshot" force the staged algorithms
-AR_ALGOS = ("ll", "ll2", "oneshot", "twoshot") + (("push",) if os.environ.get("MPIGX_ZC_MIN") else ())
+# "pull_generic": the zero-copy pull two-shot through the all-modes fold
+# kernel instead of its dedicated kernel (ar_zc_kernel)
+AR_ALGOS = ("ll", "ll2", "oneshot", "twoshot") + (("push", "pull_generic") if os.environ.get("MPIGX_ZC_MIN") else ())
 
 
 def dev(a):
@@ -56,6 +58,10 @@ class Runner:
         self.n = MPI.Comm_size(comm)
         self.fail = []
         self.ran = 0
+
+    def knob(self, name, value):
+        """Collective knob change (every rank, same value): mpigx_comm_set_knob."""
+        MPI.set_knob(self.comm, name, value)
 
     def check(self, ok, what):
         self.ran += 1
@@ -125,7 +131,7 @@ class Runner:
             coll = c["coll"]
             algos = AR_ALGOS if coll in ("allreduce", "reduce") else ("auto",)
             for algo in algos:
-                os.environ["MPIGX_ALGO"] = algo
+                self.knob("ALGO", algo)
                 for inplace in (False, True):
                     if inplace and coll in ("bcast",):
                         continue
@@ -138,7 +144,7 @@ class Runner:
                             self.check(np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (c["id"], algo, "rank0"))
                         continue
                     self.check(same_bits(got, exp), (c["id"], coll, c["dtype"], c["op"], algo, inplace))
-        os.environ.pop("MPIGX_ALGO", None)
+        self.knob("ALGO", None)
 
     def vgolden(self):
         """Gather(v)/Scatter(v)/Allgatherv/Alltoallv golden cases (MPICH) through the C ABI,
@@ -234,14 +240,14 @@ class Runner:
         for i, (dtname, opname, count) in enumerate(sizes):
             ins = make(dtname, opname, n, count, 1000 + i, edge=opname in ("MAX", "MIN"))
             for algo in AR_ALGOS:
-                os.environ["MPIGX_ALGO"] = algo
+                self.knob("ALGO", algo)
                 got = self.run("allreduce", ins, dtname, opname, count)
                 self.check(same_bits(got, M.allreduce(ins, dtname, opname)[r], dtname == "BFLOAT16"), ("oracle-allreduce", dtname, opname, count, algo))
                 root = (i + 1) % n
                 got = self.run("reduce", ins, dtname, opname, count, root=root)
                 if r == root:
                     self.check(same_bits(got, M.reduce(ins, dtname, opname, root), dtname == "BFLOAT16"), ("oracle-reduce", dtname, opname, count, algo))
-            os.environ.pop("MPIGX_ALGO", None)
+            self.knob("ALGO", None)
             got = self.run("scan", ins, dtname, opname, count)
             self.check(same_bits(got, M.scan(ins, dtname, opname)[r], dtname == "BFLOAT16"), ("oracle-scan", dtname, opname, count))
             got = self.run("exscan", ins, dtname, opname, count)
@@ -256,11 +262,11 @@ class Runner:
             got = self.run("allgather", ins1, "FLOAT", None, count)
             self.check(same_bits(got, M.allgather(ins1)[r]), ("allgather", count))
             for algo in ("direct", "sag"):  # root pull vs scatter+allgather
-                os.environ["MPIGX_BCAST"] = algo
+                self.knob("BCAST", algo)
                 for root in sorted({0, n // 2, n - 1}):
                     got = self.run("bcast", ins1, "FLOAT", None, count, root=root)
                     self.check(same_bits(got, ins1[root]), ("bcast", algo, root, count))
-            os.environ.pop("MPIGX_BCAST", None)
+            self.knob("BCAST", None)
         # bytes that are not a multiple of 16 per chunk, default algorithm choice
         for count in (262_145, 1_000_003):
             ins1 = make("UINT8_T", "BXOR", n, count, 91 + count)
@@ -274,7 +280,7 @@ class Runner:
         LL launches (both area parities reused while peers run ahead) with
         other collectives between them; vs the MPICH-pinned oracle."""
         L, n, r, cv = self.L, self.n, self.r, self.comm.val
-        os.environ["MPIGX_ALGO"] = "ll"  # LL up to the area's capacity (default: MPIGX_LL_AUTO)
+        self.knob("ALGO", "ll")  # LL up to the area's capacity (default: MPIGX_LL_AUTO)
         cases = (("UINT8_T", "BXOR", 1), ("UINT8_T", "SUM", 7), ("INT16_T", "MAX", 5), ("FLOAT", "SUM", 2),
                  ("FLOAT", "SUM", 3), ("DOUBLE", "PROD", 9), ("C_FLOAT_COMPLEX", "PROD", 17),
                  ("BFLOAT16", "SUM", 4099), ("INT64_T", "BAND", 1023), ("FLOAT", "MIN", 16384),
@@ -328,7 +334,7 @@ class Runner:
             # threshold) back to back with push two-shots, whose remote stores
             # into the peers' arenas come before any barrier: the host inserts
             # one after an LL launch (mpigx.cpp allreduce_push)
-            os.environ["MPIGX_ALGO"] = "push"
+            self.knob("ALGO", "push")
             pairs = []
             for k in range(12):
                 a = make("INT32_T", "SUM", n, 3000 + k, 4400 + k)
@@ -340,11 +346,11 @@ class Runner:
                 assert L.mpigx_allreduce(P(sb), P(db), b[r].size, M.DTYPES["FLOAT"][0], M.OPS["SUM"], cv) == 0
             assert L.mpigx_comm_synchronize(cv) == 0
             L.mpigx_comm_set_blocking(cv, 1)
-            os.environ.pop("MPIGX_ALGO", None)
+            self.knob("ALGO", None)
             for k, (a, b, sa, sb, db) in enumerate(pairs):
                 self.check(same_bits(host(sa, np.int32), M.scan(a, "INT32_T", "SUM")[r]), ("ll-push-scan", k))
                 self.check(same_bits(host(db, np.float32), M.allreduce(b, "FLOAT", "SUM")[r]), ("ll-push-ar", k))
-        os.environ.pop("MPIGX_ALGO", None)
+        self.knob("ALGO", None)
         # the first Bcast (k = 6) spreads root 6 % n's value; later ones re-send it
         self.check(bool((host(bc, np.uint8) == 6 % n).all()), "ll-burst-bcast")
 
@@ -353,7 +359,7 @@ class Runner:
         a size class run every candidate (LL / one-shot / two-shot) twice,
         then the class keeps one; every call must give MPICH's bits."""
         L, n, r, cv = self.L, self.n, self.r, self.comm.val
-        os.environ.pop("MPIGX_ALGO", None)
+        self.knob("ALGO", None)
         for k, count in ((12, 1100), (13, 2500), (16, 20000), (18, 70000)):  # FLOAT: 4.4 KB .. 280 KB
             assert (count * 4).bit_length() - 1 == k
             for i in range(10):
@@ -386,13 +392,13 @@ class Runner:
         integer / bitwise ops exact, float SUM within the stated tolerance
         2(n-1) u sum|x| (oracle sum_tolerance)."""
         n, r = self.n, self.r
-        stage = int(os.environ.get("MPIGX_STAGING_BYTES", 512 << 20))
+        stage = MPI.get_knob(self.comm, "STAGING_BYTES")
         cases = (("FLOAT", "SUM", 1_000_003), ("DOUBLE", "SUM", 65537), ("FLOAT", "MAX", 100_001),
                  ("INT32_T", "BAND", 262_147), ("INT64_T", "SUM", 50_000), ("BFLOAT16", "SUM", 40_000),
                  ("C_FLOAT_COMPLEX", "PROD", 3333), ("UINT8_T", "BXOR", 100_000), ("FLOAT", "SUM", 5))
-        os.environ["MPIGX_ALGO"] = "ring"
+        self.knob("ALGO", "ring")
         for nch in nchs:
-            os.environ["MPIGX_RING_CHANNELS"] = str(nch)
+            self.knob("RING_CHANNELS", nch)
             for i, (dt, op, count) in enumerate(cases):
                 ins = make(dt, op, n, count, 3000 + i, edge=op in ("MAX", "MIN"))
                 exp = M.fold_ring(ins, dt, op, nch, M.ring_round_elems(stage, n, dt, nch))
@@ -406,8 +412,8 @@ class Runner:
                 elif dt in ("FLOAT", "DOUBLE") and op == "SUM":
                     err = np.abs(exp.astype(np.float64) - mp.astype(np.float64))
                     self.check(bool((err <= M.sum_tolerance(ins, dt)).all()), ("ring-tolerance", dt, count))
-        os.environ.pop("MPIGX_ALGO", None)
-        os.environ.pop("MPIGX_RING_CHANNELS", None)
+        self.knob("ALGO", None)
+        self.knob("RING_CHANNELS", 1)
 
     def linear_order(self):
         MPI.set_reduce_order(self.comm, 1)
@@ -415,10 +421,10 @@ class Runner:
                                                     ("FLOAT", "MAX", 3000), ("BFLOAT16", "SUM", 9999))):
             ins = make(dtname, opname, self.n, count, 500 + i, edge=opname == "MAX")
             for algo in AR_ALGOS:
-                os.environ["MPIGX_ALGO"] = algo
+                self.knob("ALGO", algo)
                 got = self.run("allreduce", ins, dtname, opname, count)
                 self.check(same_bits(got, M.fold_linear(ins, dtname, opname), dtname == "BFLOAT16"), ("linear", dtname, opname, algo))
-        os.environ.pop("MPIGX_ALGO", None)
+        self.knob("ALGO", None)
         MPI.set_reduce_order(self.comm, 0)
 
     def errors(self):

@@ -28,6 +28,63 @@ import mpigx as MPI  # noqa: E402
 from oracle import mpich_model as M  # noqa: E402
 
 
+# every MPIGX_ALGO at 16 MiB and 1 MiB; "auto" = the size's own choice
+# (tuners included); where an algorithm cannot take a size the engine runs
+# the static choice (e.g. "ll" above its 256 KiB capacity)
+ALGOS = ("auto", "ll", "ll2", "oneshot", "twoshot", "push", "ring", "pull", "pull_generic")
+
+
+def extra(comm, r, n, f32_input, fails):
+    """The production grid (no MPIGX_MAX_BLOCKS: the default 256-block grid,
+    capped only by the ranks-per-device residency rule) through every
+    algorithm at 16 MiB and 1 MiB — whole buffers against the oracle (the
+    ring against its own association, fold_ring) — and one 1 GiB Allreduce
+    on the default path, sampled at the chunk and Rabenseifner boundaries."""
+    for mib in (16, 1):
+        count = (mib << 20) // 4
+        xs = [f32_input(q, count, 5000 + mib) for q in range(n)]
+        hs = [x.cpu().numpy() for x in xs]
+        tree = M.fold_rsag(hs, "FLOAT", "SUM")
+        for algo in ALGOS:
+            MPI.set_knob(comm, "ALGO", None if algo == "auto" else algo)
+            recv = torch.empty_like(xs[r])
+            for _ in range(3 if algo == "auto" else 1):  # auto: the tuners' sampling calls too
+                recv.zero_()
+                MPI.Allreduce_(xs[r], recv, MPI.SUM, comm)
+                got = recv.cpu().numpy()
+                if algo == "ring":
+                    stage = MPI.get_knob(comm, "STAGING_BYTES")
+                    exp = M.fold_ring(hs, "FLOAT", "SUM", 1, M.ring_round_elems(stage, n, "FLOAT", 1))
+                else:
+                    exp = tree
+                if not np.array_equal(got.view(np.uint32), exp.view(np.uint32)):
+                    bad = np.nonzero(got.view(np.uint32) != exp.view(np.uint32))[0]
+                    fails.append(("allreduce", mib, algo, int(bad.size), int(bad[0])))
+                    break
+        MPI.set_knob(comm, "ALGO", None)
+        del xs, hs
+    # 1 GiB on the default path, sampled spans
+    count = (1 << 30) // 4
+    send = f32_input(r, count, 6000)
+    recv = torch.empty_like(send)
+    MPI.Allreduce_(send, recv, MPI.SUM, comm)
+    chunk = -(-(-(-count // n)) // 4) * 4
+    spans = [(0, 1 << 15), (count - (1 << 15), count)] + \
+            [(c * chunk - 2048, c * chunk + 2048) for c in range(1, n)] + \
+            [(count // 8 * k - 1024, count // 8 * k + 1024) for k in range(1, 8)]
+    samples = {}
+    for q in range(n):
+        x = f32_input(q, count, 6000)
+        for lo, hi in spans:
+            samples.setdefault((lo, hi), []).append(x[lo:hi].cpu().numpy())
+        del x
+    for (lo, hi), ins in samples.items():
+        ref = M.fold_rsag(ins, "FLOAT", "SUM")
+        if not np.array_equal(recv[lo:hi].cpu().numpy().view(np.uint32), ref.view(np.uint32)):
+            fails.append(("allreduce-1GiB", lo, hi))
+    del send, recv
+
+
 def main():
     comm = MPI.Init()
     r, n = MPI.Comm_rank(comm), MPI.Comm_size(comm)
@@ -72,6 +129,9 @@ def main():
     if ch.value not in (0, 1):
         fails.append(("ar-tune-undecided", ch.value))
     del send, recv, again, xs
+
+    if os.environ.get("MPIGX_HEADLINE_EXTRA"):
+        extra(comm, r, n, f32_input, fails)
 
     # --- Bcast / Allgather / Alltoall at 512 MiB
     nb = 512 << 20

@@ -60,7 +60,10 @@ def test_hot_fold_kernels_have_no_scratch(rep, tmp_path):
     coll = {k: v for k, v in sizes.items() if "11fold_kernel" in k}
     assert coll, f"no fold_kernel for {rep}"
     assert all(v == 0 for v in coll.values()), {k: v for k, v in coll.items() if v}
-    # ring reduce-scatter + allgather and Scan / Exscan likewise
-    other = {k: v for k, v in sizes.items() if "11ring_kernel" in k or "11scan_kernel" in k}
+    # ring reduce-scatter + allgather, Scan / Exscan and the dedicated
+    # zero-copy two-shot (ar_zc_kernel, U vectors per thread) likewise
+    zc = {k: v for k, v in sizes.items() if "12ar_zc_kernel" in k}
+    assert len(zc) >= 5, f"ar_zc_kernel instantiations missing for {rep}"
+    other = {k: v for k, v in sizes.items() if "11ring_kernel" in k or "11scan_kernel" in k or "12ar_zc_kernel" in k}
     assert other, f"no ring/scan kernel for {rep}"
     assert all(v == 0 for v in other.values()), {k: v for k, v in other.items() if v}

@@ -207,3 +207,59 @@ def test_ring_strides():
     for n in range(2, 17):
         for st in M.ring_strides(n, 4):
             assert sorted((i * st) % n for i in range(n)) == list(range(n))
+
+
+# ---------------------------------------------------------------------------
+# Large counts: MPICH 3.3.2 recorded at 4,194,307
+# (Allreduce / Reduce: f32 SUM, f64 SUM, f32 MAX with +-0 / inf / NaN /
+# denormal edges) and 1,048,579 elements (Int64 Scan / Exscan BOR, f64 Scan
+# SUM) at n = 5 and 8 (tests/golden/make_large_golden.sh).  The fixture holds
+# sampled output spans — prefix, tail and +-64 elements around every
+# Rabenseifner block boundary — and the inputs are regenerated from their
+# splitmix64 seeds (gen_inputs.splitmix_input), so the headline-size regime
+# is pinned by MPICH itself, not by extrapolation from 1,100 elements.
+# ---------------------------------------------------------------------------
+def _large():
+    import json
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(here, "mpich_large_manifest.json")) as f:
+        cases = json.load(f)
+    return cases, np.load(os.path.join(here, "mpich_large.npz"))
+
+
+LARGE, LARGE_ARR = _large()
+
+
+@pytest.mark.parametrize("case", LARGE, ids=[c["id"] for c in LARGE])
+def test_oracle_matches_mpich_large_counts(case):
+    from gen_inputs import splitmix_input
+    n, dt, op = case["n"], case["dtype"], case["op"]
+    ins = [splitmix_input(case["kind"], case["seed"], q, case["count"], bool(case["edge"])) for q in range(n)]
+    coll = case["coll"]
+    if coll == "allreduce":
+        outs = {0: M.fold_rsag(ins, dt, op)}
+        assert case["count"] * ins[0].itemsize > 2048  # the Rabenseifner regime (what fold_rsag restates)
+    elif coll == "reduce":
+        outs = {case["root"]: M.reduce(ins, dt, op, case["root"])}
+    elif coll == "scan":
+        outs = dict(enumerate(M.scan(ins, dt, op)))
+    else:
+        outs = {q: v for q, v in enumerate(M.exscan(ins, dt, op)) if q > 0}
+    checked = 0
+    for q, full in outs.items():
+        got = LARGE_ARR[f"{case['id']}.r{q}"].view(full.dtype)
+        exp = np.concatenate([full[lo:hi] for lo, hi in case["spans"]])
+        assert same_bits(exp, got), (case["id"], q)
+        checked += 1
+    assert checked == len(outs)
+    if coll == "exscan":  # rank 0's recvbuf untouched (0xCD sentinel), as in collective.jl's Exscan!
+        assert (LARGE_ARR[f"{case['id']}.r0"] == 0xCD).all()
+
+
+def test_large_fixture_coverage():
+    kinds = {(c["coll"], c["n"]) for c in LARGE}
+    for coll in ("allreduce", "reduce", "scan", "exscan"):
+        for n in (5, 8):
+            assert (coll, n) in kinds
+    assert max(c["count"] for c in LARGE) >= 4_194_304
