@@ -50,7 +50,12 @@ function Base.Array(b::ROCBuffer{T,N}) where {T,N}
     ccall((:mpigx_memcpy, libmpigx), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t), a, b.ptr, sizeof(a))
     return a
 end
-Base.getindex(b::ROCBuffer, i::Int) = Array(b)[i]          # host copy; tests only
+function Base.getindex(b::ROCBuffer{T}, i::Int) where T   # one element, host copy (tests)
+    @boundscheck checkbounds(b, i)
+    r = Ref{T}()
+    ccall((:mpigx_memcpy, libmpigx), Cint, (Ptr{T}, Ptr{T}, Csize_t), r, b.ptr + (i - 1) * sizeof(T), sizeof(T))
+    r[]
+end
 Base.:(==)(a::ROCBuffer, b::AbstractArray) = Array(a) == b
 Base.cconvert(::Type{MPIPtr}, b::ROCBuffer) = b
 Base.unsafe_convert(::Type{MPIPtr}, b::ROCBuffer) = reinterpret(MPIPtr, b.ptr)
@@ -74,7 +79,9 @@ function engine(comm::Comm)
         MPI.Bcast!(id, 0, comm)
         # rank -> GPU binding: node-local rank (comm.jl:107 Comm_split_type SHARED)
         local_comm = MPI.Comm_split_type(comm, MPI.MPI_COMM_TYPE_SHARED, rank)
-        device = parse(Int, get(ENV, "MPIGX_DEVICE", string(MPI.Comm_rank(local_comm))))
+        local_rank = MPI.Comm_rank(local_comm)
+        MPI.free(local_comm)  # only its rank is needed (comm.jl:107)
+        device = parse(Int, get(ENV, "MPIGX_DEVICE", string(local_rank)))
         h = Ref{Ptr{Cvoid}}(C_NULL)
         @mpichk ccall((:mpigx_comm_init_rank, libmpigx), Cint, (Ptr{Ptr{Cvoid}}, Cint, Ptr{UInt8}, Cint, Cint),
                       h, MPI.Comm_size(comm), id, rank, device)
@@ -124,6 +131,36 @@ function Alltoall!(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Integer
     recvbuf
 end
 
+# ---------------------------------------------------------------------------
+# op handles on the engine (collective.jl:698-700 passes `op` straight to
+# libmpi): built-in handles are the same MPICH values in both libraries; an
+# `MPI.Op(f, T)` made by the REFERENCE (operators.jl:72-88) holds a libmpi
+# handle from MPI_Op_create plus, in `fptr`, the @cfunction of its OpWrapper
+# — an MPI_User_function, exactly what mpigx_op_create takes.  Such an op is
+# re-registered with libmpigx once (commutativity from libmpi's
+# MPI_Op_commutative) and the engine handle is cached for the Op's lifetime.
+# libmpigx's own handles (DeviceOp below, csrc/handles.hpp space
+# 0x3c000000) pass through; a foreign handle with no function (fptr ===
+# nothing) is passed as is and libmpigx rejects it with MPI_ERR_OP.
+# ---------------------------------------------------------------------------
+const ENGINE_OPS = IdDict{Op,Cint}()
+is_engine_handle(v) = (UInt32(reinterpret(UInt32, Cint(v))) & 0xfc000000) == 0x3c000000
+function engine_op(op::Op)
+    (op.fptr === nothing || is_engine_handle(op.val)) && return Cint(op.val)
+    get!(ENGINE_OPS, op) do
+        commute = Ref{Cint}(0)
+        @mpichk ccall((:MPI_Op_commutative, MPI.libmpi), Cint, (MPI_Op, Ptr{Cint}), op.val, commute)
+        h = Ref{Cint}(0)
+        @mpichk ccall((:mpigx_op_create, libmpigx), Cint, (Ptr{Cvoid}, Cint, Ptr{Cint}),
+                      Base.unsafe_convert(Ptr{Cvoid}, op.fptr), commute[], h)
+        # the engine handle goes when the reference's Op is freed (operators.jl:47-53)
+        finalizer(o -> (h2 = Ref(pop!(ENGINE_OPS, o, Cint(0))); h2[] != 0 &&
+                        ccall((:mpigx_op_free, libmpigx), Cint, (Ptr{Cint},), h2)), op)
+        h[]
+    end
+end
+engine_op(op::MPI_Op) = Cint(op)
+
 # collective.jl:605-618 (recvbuf may be `nothing` on non-roots)
 function Reduce!(sendbuf::DeviceOrSentinel, recvbuf::Union{ROCBuffer,Nothing}, count::Integer,
                  op::Union{Op,MPI_Op}, root::Integer, comm::Comm)
@@ -136,7 +173,7 @@ function Reduce!(sendbuf::DeviceOrSentinel, recvbuf::Union{ROCBuffer,Nothing}, c
     T = sendbuf isa SentinelPtr ? eltype(recvbuf) : eltype(sendbuf)
     @mpichk ccall((:mpigx_reduce, libmpigx), Cint,
                   (MPIPtr, MPIPtr, Cint, MPI_Datatype, MPI_Op, Cint, Ptr{Cvoid}),
-                  sendbuf, recvbuf, count, Datatype(T), op, root, engine(comm))
+                  sendbuf, recvbuf, count, Datatype(T), engine_op(op), root, engine(comm))
     recvbuf
 end
 
@@ -149,7 +186,7 @@ function Allreduce!(sendbuf::DeviceOrSentinel, recvbuf::ROCBuffer, count::Intege
     T = eltype(recvbuf)
     @mpichk ccall((:mpigx_allreduce, libmpigx), Cint,
                   (MPIPtr, MPIPtr, Cint, MPI_Datatype, MPI_Op, Ptr{Cvoid}),
-                  sendbuf, recvbuf, count, Datatype(T), op, engine(comm))
+                  sendbuf, recvbuf, count, Datatype(T), engine_op(op), engine(comm))
     recvbuf
 end
 
@@ -160,7 +197,7 @@ for (jl, c) in ((:Scan!, :mpigx_scan), (:Exscan!, :mpigx_exscan))
         T = eltype(recvbuf)
         @mpichk ccall(($(QuoteNode(c)), libmpigx), Cint,
                       (MPIPtr, MPIPtr, Cint, MPI_Datatype, MPI_Op, Ptr{Cvoid}),
-                      sendbuf, recvbuf, count, Datatype(T), op, engine(comm))
+                      sendbuf, recvbuf, count, Datatype(T), engine_op(op), engine(comm))
         recvbuf
     end
 end

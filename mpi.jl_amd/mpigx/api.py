@@ -183,15 +183,22 @@ def _kind(T) -> str:
 # Op (src/operators.jl)
 # ---------------------------------------------------------------------------
 class Op:
-    """Built-in op handle, or a user function (OpWrapper, operators.jl:56-88)."""
-    __slots__ = ("val", "name", "fn", "iscommutative")
+    """Built-in op handle, or a user function (OpWrapper, operators.jl:56-88).
 
-    def __init__(self, f, T=None, iscommutative=False, *, _val=None, _name=None):
+    `fptr` mirrors MPI.jl's `Op.fptr` (operators.jl:20, :77-79): the
+    MPI_User_function of an op created in libmpi (`libmpi_op`); a device-buffer
+    call re-registers it with libmpigx (`_op_val`)."""
+    __slots__ = ("val", "name", "fn", "iscommutative", "fptr")
+
+    def __init__(self, f, T=None, iscommutative=False, *, _val=None, _name=None, _fptr=None):
+        self.fptr = _fptr
         if _val is not None:
-            self.val, self.name, self.fn, self.iscommutative = _val, _name, None, True
+            self.val, self.name, self.fn = _val, _name, None
+            self.iscommutative = True if _fptr is None else bool(iscommutative)
             return
         if isinstance(f, Op):
             self.val, self.name, self.fn, self.iscommutative = f.val, f.name, f.fn, f.iscommutative
+            self.fptr = f.fptr
             return
         b = _builtin_for(f, T)
         if b is not None:
@@ -206,6 +213,13 @@ class Op:
 
 def _op(name, val):
     return Op(None, _val=val, _name=name)
+
+
+def libmpi_op(handle, fptr, iscommutative=False, name="libmpi"):
+    """An op as MPI.jl's `MPI.Op(f, T)` holds it (operators.jl:72-88): the
+    handle libmpi's MPI_Op_create returned and the MPI_User_function pointer
+    (a ctypes USER_FN object or a raw address) it was created from."""
+    return Op(None, None, iscommutative, _val=int(handle), _name=name, _fptr=fptr)
 
 
 OP_NULL = _op("OP_NULL", C.MPI_OP_NULL)
@@ -603,10 +617,40 @@ def _call(coll, buf, comm, *args):
     _check(rc)
 
 
+_ENGINE_TAG, _ENGINE_MASK = 0x3C000000, 0xFC000000  # csrc/handles.hpp: libmpigx's own handle space
+_LIBMPI_OPS = {}  # id(Op) -> (Op, engine handle, function object)
+
+
+def _engine_user_op(opx):
+    """A libmpi user op (handle + MPI_User_function) on device buffers: the
+    same function registered with libmpigx once (mpigx_op_create takes the
+    MPI_User_function ABI), as the Julia glue's engine_op does."""
+    from ._lib import USER_FN
+    hit = _LIBMPI_OPS.get(id(opx))
+    if hit is not None and hit[0] is opx:
+        return hit[1]
+    f = opx.fptr if isinstance(opx.fptr, USER_FN) else USER_FN(int(opx.fptr))
+    commute = int(bool(opx.iscommutative))
+    if hostmpi.available():  # the reference asks libmpi (MPI_Op_commutative)
+        c = ctypes.c_int(0)
+        if hostmpi.lib().MPI_Op_commutative(ctypes.c_int(opx.val), ctypes.byref(c)) == 0:
+            commute = c.value
+    h = ctypes.c_int(0)
+    _check(lib().mpigx_op_create(f, commute, ctypes.byref(h)))
+    _LIBMPI_OPS[id(opx)] = (opx, h.value, f)
+    return h.value
+
+
 def _op_val(opx, buf):
     """Built-in handle, or an MPI_Op_create'd user function: libmpi's for host
-    buffers, libmpigx's device-callback op for device buffers."""
+    buffers, libmpigx's device-callback op for device buffers.  A libmpi op
+    carrying its function pointer (libmpi_op) is re-registered with libmpigx
+    for device buffers; a foreign handle without one goes through unchanged
+    and libmpigx rejects it (MPI_ERR_OP)."""
     if opx.val is not None:
+        if (opx.fptr is not None and not _is_host(buf) and buf is not IN_PLACE
+                and (opx.val & _ENGINE_MASK) != _ENGINE_TAG):
+            return _engine_user_op(opx)
         return opx.val
     if _is_host(buf):
         return hostmpi.user_op(opx.fn, _unwrap(buf).dtype, opx.iscommutative)

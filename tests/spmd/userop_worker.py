@@ -25,7 +25,11 @@ import numpy as np  # noqa: E402
 import mpigx as MPI  # noqa: E402
 
 DEVICE = os.environ.get("MPIGX_TEST_ARRAYTYPE", "") == "ROCArray"
-HOSTCB = os.environ.get("USEROP_HOSTCB", "") == "1"  # device buffers, host-staged MPI_User_function
+HOSTCB = os.environ.get("USEROP_HOSTCB", "") in ("1", "libmpi")  # device buffers, host-staged MPI_User_function
+# "libmpi": the op reaches the engine as MPI.jl's MPI.Op(f, T) holds it — a
+# libmpi handle (MPICH's user-op handle format) plus the MPI_User_function
+# pointer — and the API re-registers that function with libmpigx
+LIBMPI = os.environ.get("USEROP_HOSTCB", "") == "libmpi"
 if DEVICE:
     import torch
 
@@ -84,8 +88,44 @@ def host_cb_op(fn):
     return MPI.Op(None, _val=h.value, _name="hostcb")
 
 
+_MPICH_USER_OP = [0x98000000]  # HANDLE_KIND_DIRECT | MPIR_OP: what MPICH's MPI_Op_create returns
+
+
+def libmpi_style_op(fn):
+    """(libmpi handle, MPI_User_function) as MPI.jl's Op(f, T) carries them
+    (operators.jl:77-88); NOT registered with libmpigx here."""
+    from mpigx._lib import USER_FN
+
+    def cb(invec, inoutvec, plen, pdt):
+        sz = ctypes.c_longlong(0)
+        MPI.lib().mpigx_type_size_x(pdt[0], ctypes.byref(sz))
+        nb = plen[0] * sz.value
+        a = np.ctypeslib.as_array((ctypes.c_char * nb).from_address(invec)).view(np.int64)
+        b = np.ctypeslib.as_array((ctypes.c_char * nb).from_address(inoutvec)).view(np.int64)
+        b[:] = fn(a, b)
+
+    f = USER_FN(cb)
+    _keep.append(f)
+    _MPICH_USER_OP[0] += 1
+    return MPI.libmpi_op(_MPICH_USER_OP[0], f, iscommutative=False)
+
+
 def op_of(fn):
+    if LIBMPI:
+        return libmpi_style_op(fn)
     return host_cb_op(fn) if HOSTCB else MPI.Op(fn, np.int64)
+
+
+def foreign_handle_rejected():
+    """A libmpi handle WITHOUT its function cannot run on the engine: MPI_ERR_OP."""
+    x = dev(np.arange(4, dtype=np.int64))
+    y = dev(np.zeros(4, np.int64))
+    try:
+        MPI.Allreduce_(x, y, MPI.Op(None, _val=0x98000042, _name="foreign"), comm)
+    except MPI.MPIError as e:
+        assert e.code == 9, e.code
+        return
+    raise AssertionError("foreign op handle accepted")
 
 
 def cases():
@@ -159,6 +199,8 @@ def large_cases(opc, pair):
 failed = None
 try:
     cases()
+    if LIBMPI:
+        foreign_handle_rejected()
     MPI.Barrier(comm)
 except Exception:  # noqa: BLE001
     failed = traceback.format_exc()

@@ -174,3 +174,26 @@ def test_own_handles_never_alias_mpich():
     freed = t.value
     assert L.mpigx_type_free(ctypes.byref(t)) == 0
     assert L.mpigx_type_size(freed, ctypes.byref(sz)) == C.MPI_ERR_TYPE
+
+
+def test_knob_constants_match_the_python_mirror():
+    """include/mpigx.h MPIGX_KNOB_* / MPIGX_ALGO_* == mpigx.KNOBS / mpigx.ALGOS."""
+    txt = re.sub(r"/\*.*?\*/", "", header_text(), flags=re.S)
+    d = {k: int(v) for k, v in re.findall(r"#define\s+(MPIGX_\w+)\s+(-?\d+)\s*$", txt, flags=re.M)}
+    knobs = {k[len("MPIGX_KNOB_"):]: v for k, v in d.items() if k.startswith("MPIGX_KNOB_") and k != "MPIGX_KNOB_COUNT"}
+    assert knobs == mpigx.KNOBS
+    assert d["MPIGX_KNOB_COUNT"] == len(knobs)
+    algos = {k[len("MPIGX_ALGO_"):].lower(): v for k, v in d.items() if k.startswith("MPIGX_ALGO_")}
+    assert {("auto" if k == "auto" else k): v for k, v in algos.items()} == \
+        {k: v for k, v in mpigx.ALGOS.items() if k}
+
+
+def test_libmpi_op_carries_its_function():
+    """MPI.jl's Op(val, fptr) (operators.jl:20, :77-79): the mirror keeps both,
+    and copies keep the function (the engine re-registers it, api._op_val)."""
+    from mpigx._lib import USER_FN
+    f = USER_FN(lambda a, b, n, t: None)
+    op = mpigx.libmpi_op(0x98000001, f, iscommutative=True)
+    assert op.val == 0x98000001 and op.fptr is f and op.iscommutative
+    assert mpigx.Op(op).fptr is f
+    assert mpigx.SUM.fptr is None

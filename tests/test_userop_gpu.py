@@ -5,7 +5,10 @@ contiguous derived pair type through Allreduce / Reduce / Scan / Exscan — on
 ROCm tensors must reproduce MPICH's MPI_Op_create results
 (tests/golden/userop_golden.json) through BOTH engine paths: the device
 callback (torch ops on device pointers) and the host-staged
-MPI_User_function callback (what MPI.jl's @cfunction(OpWrapper) binds)."""
+MPI_User_function callback (what MPI.jl's @cfunction(OpWrapper) binds) —
+and, "libmpi", an op handed over as the reference's MPI.Op(f, T) holds it (a
+libmpi handle plus that function pointer), which the API re-registers with
+libmpigx; the same handle without a function stays MPI_ERR_OP."""
 import json
 import os
 
@@ -20,7 +23,7 @@ ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_MAX_BLOCKS"
 
 
 @pytest.mark.parametrize("n", [2, 3, 4])
-@pytest.mark.parametrize("hostcb", ["0", "1"])
+@pytest.mark.parametrize("hostcb", ["0", "1", "libmpi"])
 def test_user_ops_device_match_mpich(n, hostcb, tmp_path):
     env = dict(ENV, UO_OUT=str(tmp_path / "uo"), USEROP_HOSTCB=hostcb)
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "userop_worker.py"), n, timeout=300, extra_env=env)
