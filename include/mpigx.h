@@ -173,7 +173,7 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
 #define MPIGX_ALGO_RING 6     /* "ring" */
 #define MPIGX_ALGO_PULL 7     /* "pull": the zero-copy pull two-shot (no pull/push tuning) */
 #define MPIGX_ALGO_PULL_GENERIC 8 /* "pull_generic": the same through the all-modes fold kernel
-                                     (one vector per thread in flight; comparison only) */
+                                     (fewer vectors per thread in flight; comparison only) */
 int mpigx_comm_set_knob(mpigx_comm_t comm, int knob, long long value);
 int mpigx_comm_get_knob(mpigx_comm_t comm, int knob, long long *value);
 

@@ -7,10 +7,14 @@
 
 namespace mpigx {
 
-template <int NMAX>
+// NMAX = n rounded up to a power of two (2, 4, 8, 16) and U = 16 / NMAX
+// 16-B vectors per peer per thread in flight (block_gather_u): ~16 loads
+// outstanding per thread at every rank count (one per peer held the n = 2
+// same-device Allgather at a third of HBM, VERDICT r02 / DESIGN §5).
+template <int NMAX, int U>
 __device__ __forceinline__ int copy_body(const CopyArgs& A);
 
-template <int NMAX>
+template <int NMAX, int U>
 __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
   // per-rank arrays are indexed at run time: staged in LDS (kernels.hpp)
   __shared__ CopyArgs sA;
@@ -19,7 +23,7 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(CopyArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
-  const int ab = copy_body<NMAX>(sA);
+  const int ab = copy_body<NMAX, U>(sA);
   signal_done(sA.pv, ab);
 }
 
@@ -30,7 +34,16 @@ __device__ __forceinline__ void chunk_slice(const CopyArgs& A, int k, int b, lon
   *hi = lmin(*lo + A.slice, c1);
 }
 
-template <int NMAX>
+// one source -> one destination with U * 16 B per thread in flight
+template <int U>
+__device__ __forceinline__ void block_copy_u(char* dst, const char* src, long long len) {
+  char* d[1] = {dst};
+  const char* s[1] = {src};
+  const long long l[1] = {len};
+  block_gather_u<1, U>(d, s, l, 1);
+}
+
+template <int NMAX, int U>
 __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the zero-copy abort verdict
   const PeerView& pv = A.pv;
   const int b = blockIdx.x, r = pv.rank, n = pv.n;
@@ -106,7 +119,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     // its links by itself (one reader per link)
     if (r == A.root) block_copy(mine + lo, send + lo, len);
     if (!rank_barrier(pv, ep++)) return 0;
-    if (r != A.root) block_copy(recv + lo, pv.stage[A.root] + lo, len);
+    if (r != A.root) block_copy_u<2 * U>(recv + lo, pv.stage[A.root] + lo, len);
     rank_barrier(pv, ep++);
     return 0;
   }
@@ -147,7 +160,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
           m = j + 1;
         }
       }
-      block_gather<NMAX>(dsts, srcs, lens, m);
+      block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     }
     rank_barrier(pv, ep++);
     return 0;
@@ -170,7 +183,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
         m = j + 1;
       }
     }
-    block_gather<NMAX>(dsts, srcs, lens, m);
+    block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     rank_barrier(pv, ep++);
     return 0;
   }
@@ -195,7 +208,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
           m = j + 1;
         }
       }
-      block_gather<NMAX>(dsts, srcs, lens, m);
+      block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     }
     rank_barrier(pv, ep++, &ab);
     return ab;
@@ -204,7 +217,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     // every non-root pulls the root's buffer (its IPC mapping) into its own
     int ab;
     if (!zc_enter(pv, ep++, &ab)) return 0;
-    if (!ab && r != A.root) block_copy(recv + lo, A.zsrc[A.root] + lo, len);
+    if (!ab && r != A.root) block_copy_u<2 * U>(recv + lo, A.zsrc[A.root] + lo, len);
     rank_barrier(pv, ep++, &ab);
     return ab;
   }
@@ -237,7 +250,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
           m = j + 1;
         }
       }
-      block_gather<NMAX>(dsts, srcs, lens, m);
+      block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     }
     rank_barrier(pv, ep++, &ab);
     return ab;
@@ -261,7 +274,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
         m = j + 1;
       }
     }
-    block_gather<NMAX>(dsts, srcs, lens, m);
+    block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     }
     rank_barrier(pv, ep++, &ab);  // nobody reads my sendbuf any more
     return ab;
@@ -284,7 +297,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
       m = j + 1;
     }
   }
-  block_gather<NMAX>(dsts, srcs, lens, m);
+  block_gather_u<NMAX, U>(dsts, srcs, lens, m);
   rank_barrier(pv, ep++);
   return 0;
 }
@@ -303,7 +316,7 @@ __device__ __forceinline__ void round_slice(long long L, long long off, long lon
   *hi = lmin(*lo + sl, len);
 }
 
-template <int NMAX>
+template <int NMAX, int U>
 __device__ __forceinline__ void vx_body(const VArgs& A) {
   const PeerView& pv = A.pv;
   const int b = blockIdx.x, r = pv.rank, n = pv.n;
@@ -334,21 +347,22 @@ __device__ __forceinline__ void vx_body(const VArgs& A) {
       m = j + 1;
     }
   }
-  block_gather<NMAX>(dsts, srcs, lens, m);
+  block_gather_u<NMAX, U>(dsts, srcs, lens, m);
   rank_barrier(pv, ep++);
 }
 
-template <int NMAX>
+template <int NMAX, int U>
 __global__ __launch_bounds__(kThreads) void vx_kernel(VArgs A) {
-  vx_body<NMAX>(A);
+  vx_body<NMAX, U>(A);
   signal_done(A.pv);
 }
 
 hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a) {
-  if (a.pv.n <= 8)
-    hipLaunchKernelGGL(vx_kernel<8>, grid, dim3(kThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL(vx_kernel<16>, grid, dim3(kThreads), 0, s, a);
+  const int n = a.pv.n;
+  if (n <= 2) hipLaunchKernelGGL((vx_kernel<2, 8>), grid, dim3(kThreads), 0, s, a);
+  else if (n <= 4) hipLaunchKernelGGL((vx_kernel<4, 4>), grid, dim3(kThreads), 0, s, a);
+  else if (n <= 8) hipLaunchKernelGGL((vx_kernel<8, 2>), grid, dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL((vx_kernel<16, 1>), grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -420,30 +434,40 @@ hipError_t launch_pack(hipStream_t s, const PackArgs& a) {
 }
 
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a) {
-  if (a.pv.n <= 8)
-    hipLaunchKernelGGL(copy_kernel<8>, grid, dim3(kThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL(copy_kernel<16>, grid, dim3(kThreads), 0, s, a);
+  const int n = a.pv.n;
+  if (n <= 2) hipLaunchKernelGGL((copy_kernel<2, 8>), grid, dim3(kThreads), 0, s, a);
+  else if (n <= 4) hipLaunchKernelGGL((copy_kernel<4, 4>), grid, dim3(kThreads), 0, s, a);
+  else if (n <= 8) hipLaunchKernelGGL((copy_kernel<8, 2>), grid, dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL((copy_kernel<16, 1>), grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
 // Resident 256-thread blocks per CU of the byte movers that spin on their
-// peers (copy_kernel, vx_kernel) for an nmax (8 or 16); 0 if unknown.
-int occupancy_copy(int nmax) {
-  int a = 0, b = 0;
-  hipError_t e1, e2;
-  if (nmax <= 8) {
-    e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, copy_kernel<8>, kThreads, 0);
-    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, vx_kernel<8>, kThreads, 0);
-  } else {
-    e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, copy_kernel<16>, kThreads, 0);
-    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, vx_kernel<16>, kThreads, 0);
-  }
-  if (e1 != hipSuccess || e2 != hipSuccess) {
+// peers (copy_kernel, vx_kernel) for an nmax (8: n <= 8, 16); 0 if unknown.
+template <class K>
+int occ_k(K k) {
+  int v = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, k, kThreads, 0) != hipSuccess) {
     (void)hipGetLastError();
     return 0;
   }
-  return a < b ? a : b;
+  return v;
+}
+int occupancy_copy(int nmax) {
+  int m = 1 << 20;
+  auto lo = [&](int v) { m = v < m ? v : m; };
+  if (nmax <= 8) {
+    lo(occ_k(copy_kernel<2, 8>));
+    lo(occ_k(copy_kernel<4, 4>));
+    lo(occ_k(copy_kernel<8, 2>));
+    lo(occ_k(vx_kernel<2, 8>));
+    lo(occ_k(vx_kernel<4, 4>));
+    lo(occ_k(vx_kernel<8, 2>));
+  } else {
+    lo(occ_k(copy_kernel<16, 1>));
+    lo(occ_k(vx_kernel<16, 1>));
+  }
+  return m;
 }
 
 }  // namespace mpigx

@@ -444,7 +444,7 @@ __device__ __forceinline__ bool fold_leaves(const FoldArgs& A, long long e, Leav
     if constexpr (SHAPE == SH_PRE) {
 #pragma unroll
       for (int s = 0; s < NMAX / 2; ++s)
-        if (s < A.rem) vapply<OP, T, W>(v[s], v[s], L.u[s]);  // inout = odd rank 2s+1
+        if (s < A.rem) vapply<OP, T, W>(v[s], v[s], L.u[s]);  // inout = even rank 2s (MPICH Reduce pre-step)
     }
     if constexpr (!role_sensitive<OP, T>::v) {
       fold_tree<OP, T, NMAX, W, 0>(nt, v);
@@ -492,11 +492,22 @@ __device__ __forceinline__ void fold_elems(const FoldArgs& A, const T* const* sr
 // Fold [lo, hi) (element indices into the sources) into out1 (and out2 if
 // non-null), the whole block cooperating.  lo is a multiple of the vector
 // width; `vec` says whether every pointer involved is 16-byte aligned.
-template <class OP, class T, int NMAX, int SCHED, int SHAPE>
+template <class OP, class T, int NMAX, int SCHED, int SHAPE, int U>
+__device__ __forceinline__ void fold_span(const FoldArgs& A, const T* const* src, const T* const* src2, long long lo,
+                                          long long hi, T* out, T* out2);
+// U > 1 (block-cooperative callers): the aligned range goes through fold_span
+// (U vectors' leaves in flight per thread)
+template <class OP, class T, int NMAX, int SCHED, int SHAPE, int U = 1>
 __device__ __forceinline__ void fold_range(const FoldArgs& A, const T* const* src, const T* const* src2,
                                            long long lo, long long hi, T* out1, T* out2, bool vec,
                                            long long tid, long long nthr) {
   constexpr int W = VecW<T>::v;
+  if constexpr (U > 1) {
+    if (vec) {
+      fold_span<OP, T, NMAX, SCHED, SHAPE, U>(A, src, src2, lo, hi, out1, out2);
+      return;
+    }
+  }
   if (vec) {
     const long long nv = (hi - lo) / W;
     for (long long i = tid; i < nv; i += nthr) {
@@ -640,9 +651,9 @@ __device__ __forceinline__ void block_gather_u(char* const (&dst)[NMAX], const c
 // U * (ntree + rem) leaf loads of a thread are issued before any arithmetic
 // (fold_range keeps one vector's leaves in flight).  lo is a multiple of the
 // vector width and every pointer is 16-B aligned (the caller checked).
-template <class OP, class T, int NMAX, int SHAPE, int U>
+template <class OP, class T, int NMAX, int SCHED, int SHAPE, int U>
 __device__ __forceinline__ void fold_span(const FoldArgs& A, const T* const* src, const T* const* src2, long long lo,
-                                          long long hi, T* out) {
+                                          long long hi, T* out, T* out2) {
   constexpr int W = VecW<T>::v;
   const long long tid = threadIdx.x, nt = blockDim.x;
   const long long nv = (hi - lo) / W;
@@ -650,26 +661,34 @@ __device__ __forceinline__ void fold_span(const FoldArgs& A, const T* const* src
   for (; v0 + (long long)(U - 1) * nt < nv; v0 += U * nt) {
     Leaves<T, NMAX, SHAPE, W> L[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) load_leaves<T, NMAX, S_TREE, SHAPE, W>(A, src, src2, lo + (v0 + u * nt) * W, L[u]);
+    for (int u = 0; u < U; ++u) load_leaves<T, NMAX, SCHED, SHAPE, W>(A, src, src2, lo + (v0 + u * nt) * W, L[u]);
     unsigned strad = 0;  // vectors straddling a Rabenseifner block boundary
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long e = lo + (v0 + u * nt) * W;
       Vec<T, W> r;
-      if (fold_leaves<OP, T, NMAX, S_TREE, SHAPE, W>(A, e, L[u], r)) stv<T, W>(out + e, r);
-      else strad |= 1u << u;
+      if (fold_leaves<OP, T, NMAX, SCHED, SHAPE, W>(A, e, L[u], r)) {
+        stv<T, W>(out + e, r);
+        if (out2) stv<T, W>(out2 + e, r);
+      } else {
+        strad |= 1u << u;
+      }
     }
 #pragma unroll 1
     for (int u = 0; u < U; ++u)
-      if ((strad >> u) & 1u) fold_elems<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, lo + (v0 + u * nt) * W, W, out, nullptr);
+      if ((strad >> u) & 1u) fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, lo + (v0 + u * nt) * W, W, out, out2);
   }
   for (; v0 < nv; v0 += nt) {
     const long long e = lo + v0 * W;
     Vec<T, W> r;
-    if (fold_at<OP, T, NMAX, S_TREE, SHAPE, W>(A, src, src2, e, r)) stv<T, W>(out + e, r);
-    else fold_elems<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, e, W, out, nullptr);
+    if (fold_at<OP, T, NMAX, SCHED, SHAPE, W>(A, src, src2, e, r)) {
+      stv<T, W>(out + e, r);
+      if (out2) stv<T, W>(out2 + e, r);
+    } else {
+      fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, e, W, out, out2);
+    }
   }
-  for (long long e = lo + nv * W + tid; e < hi; e += nt) fold_elems<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, e, 1, out, nullptr);
+  for (long long e = lo + nv * W + tid; e < hi; e += nt) fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, e, 1, out, out2);
 }
 
 // ---------------------------------------------------------------------------

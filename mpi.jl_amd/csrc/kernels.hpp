@@ -134,6 +134,10 @@ __global__ __launch_bounds__(kThreads) void fold_local_kernel(FoldArgs A) {
 
 template <class OP, class T, int NMAX, int SCHED>
 __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the zero-copy abort verdict
+  // two vectors per thread in flight in every fold and gather of the
+  // collective modes at n <= 8 (ar_zc_kernel goes further for the headline
+  // zero-copy two-shot); NMAX 16 (n = 9..16) keeps one (VGPRs)
+  constexpr int FU = NMAX <= 8 ? 2 : 1;
   const T* const* src = reinterpret_cast<const T* const*>(A.src);
   const T* const* src2 = reinterpret_cast<const T* const*>(A.src2);
   const PeerView& pv = A.pv;
@@ -166,7 +170,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
 #pragma unroll
     for (int s = 0; s < NMAX / 2; ++s)
       if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
-    fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
+    fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
     }
     stamp(pv, 2);
     if (!rank_barrier(pv, ep++, &ab)) return 0;  // every reduced chunk is in its owner's recvbuf
@@ -189,7 +193,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
         lens[j] = (h2 - l2) * es;
       }
     }
-    block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
     }
     stamp(pv, 4);
     rank_barrier(pv, ep++, &ab);  // nobody reads my buffers any more
@@ -218,9 +222,9 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       // (two calls, not a select of the output pointer: selecting between
       // recv and the arena made the compiler copy FoldArgs to scratch)
       if (r == A.root)
-        fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, vec && recv_vec, tid, nt);
+        fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, recv, nullptr, vec && recv_vec, tid, nt);
       else  // arena: element e of my chunk at e - c0 (c0 is a multiple of the vector width)
-        fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, mine - c0, nullptr, vec, tid, nt);
+        fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, mine - c0, nullptr, vec, tid, nt);
     }
     if (!rank_barrier(pv, ep++, &ab)) return 0;
     if (!ab && r == A.root) {
@@ -241,7 +245,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
           lens[j] = (h2 - l2) * es;
         }
       }
-      block_gather<NMAX>(dsts, srcs, lens, n - 1);
+      block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
     }
     rank_barrier(pv, ep++, &ab);  // nobody reads my sendbuf / arena any more
     return ab;
@@ -274,7 +278,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
         lens[j] = (h2 - l2) * es;
       }
     }
-    block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
     stamp(pv, 2);
     // phase 2 writes into the peers' recvbufs through the view's mappings:
     // the barrier checks every rank uses the same view (zc_enter)
@@ -293,7 +297,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
 #pragma unroll
     for (int s = 0; s < NMAX / 2; ++s)
       if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
-    fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
+    fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, recv, nullptr, vec, tid, nt);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NMAX; ++j) {
@@ -307,7 +311,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
         lens[j] = (hi - lo) * es;
       }
     }
-    block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
     }
     stamp(pv, 4);
     rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
@@ -327,7 +331,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
                      pv.n, pv.rank, pv.timeout_ticks, pv.err))
       return 0;
     if (A.mode == M_AR_LL || pv.rank == A.root)
-      fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
+      fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
     return 0;
   }
 
@@ -383,7 +387,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
 #pragma unroll
     for (int q = 0; q < NMAX / 2; ++q)
       if (q < A.rem) vec &= ((uintptr_t)A.src2[q] & 15) == 0;
-    fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, rlo, rhi, recv, nullptr, vec, tid, nt);
+    fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, rlo, rhi, recv, nullptr, vec, tid, nt);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // allgather: my reduced slice -> every rank; slice b of chunk p <- rank p
@@ -410,7 +414,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     block_copy((char*)(mine + lo), send + lo * es, (hi - lo) * es);
     if (!rank_barrier(pv, ep++)) return 0;
     if (A.mode == M_AR_ONESHOT || pv.rank == A.root)
-      fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
+      fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
     rank_barrier(pv, ep++);
     return 0;
   }
@@ -431,9 +435,9 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     // staging (for the peers' gather) and straight into my recvbuf.
     const bool want_recv = (A.mode == M_AR_TWOSHOT) || (r == A.root);
     if (want_recv)
-      fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, recv, mine, recv_vec, tid, nt);
+      fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, recv, mine, recv_vec, tid, nt);
     else
-      fold_range<OP, T, NMAX, SCHED, SH_PRE>(A, src, src2, lo, hi, mine, nullptr, true, tid, nt);
+      fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, mine, nullptr, true, tid, nt);
   }
   (void)W;
   if (!rank_barrier(pv, ep++)) return 0;
@@ -457,7 +461,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
         lens[j] = (hi - lo) * es;
       }
     }
-    block_gather<NMAX>(dsts, srcs, lens, n - 1);
+    block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
   }
   rank_barrier(pv, ep++);
   return 0;
@@ -517,7 +521,7 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
       for (int s = 0; s < NMAX / 2; ++s)
         if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
     }
-    if (vec) fold_span<OP, T, NMAX, SHAPE, U>(A, src, src2, lo, hi, recv);
+    if (vec) fold_span<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, hi, recv, nullptr);
     else fold_range<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, lo, hi, recv, nullptr, false, tid, nt);
   }
   stamp(pv, 2);
