@@ -178,13 +178,14 @@ int mpigx_comm_set_knob(mpigx_comm_t comm, int knob, long long value);
 int mpigx_comm_get_knob(mpigx_comm_t comm, int knob, long long *value);
 
 /* Ranks sharing one GPU.  Collective kernels spin on their peers, so every
- * rank's grid must run at once: init caps MPIGX_KNOB_MAX_BLOCKS so that the
- * grids of the most-loaded device fit its compute units at the collective
- * kernels' occupancy, and fails with MPIGX_ERR_OTHER when more than
- * MPIGX_MAX_RANKS_PER_DEVICE (environment, default 10) ranks share a device
- * (more rank processes than that did not all get hardware queues at once on
- * MI355X: some ranks' kernels never started while their peers spun).
- * *ranks = ranks on the most-loaded device, *cap = the grid cap in force. */
+ * rank's grid must run at once: each launch caps its grid at
+ * CUs x (resident blocks per CU of THAT kernel, from the occupancy API) /
+ * (ranks on the most-loaded device), identical on every rank; init fails
+ * with MPIGX_ERR_OTHER when more than MPIGX_MAX_RANKS_PER_DEVICE (environment,
+ * default 10) ranks share a device (beyond that, some rank processes' kernels
+ * were seen not to start while their peers spun).  *ranks = ranks on the
+ * most-loaded device, *cap = compute units per rank there (a kernel's grid
+ * cap is *cap x its resident blocks per CU). */
 int mpigx_comm_device_share(mpigx_comm_t comm, int *ranks, int *cap);
 
 /* Diagnostic: per-block phase timestamps of the collective kernels (100 MHz

@@ -443,7 +443,7 @@ hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a) {
 }
 
 // Resident 256-thread blocks per CU of the byte movers that spin on their
-// peers (copy_kernel, vx_kernel) for an nmax (8: n <= 8, 16); 0 if unknown.
+// peers (copy_kernel, vx_kernel) of an n-rank communicator; 0 if unknown.
 template <class K>
 int occ_k(K k) {
   int v = 0;
@@ -453,21 +453,17 @@ int occ_k(K k) {
   }
   return v;
 }
-int occupancy_copy(int nmax) {
-  int m = 1 << 20;
-  auto lo = [&](int v) { m = v < m ? v : m; };
-  if (nmax <= 8) {
-    lo(occ_k(copy_kernel<2, 8>));
-    lo(occ_k(copy_kernel<4, 4>));
-    lo(occ_k(copy_kernel<8, 2>));
-    lo(occ_k(vx_kernel<2, 8>));
-    lo(occ_k(vx_kernel<4, 4>));
-    lo(occ_k(vx_kernel<8, 2>));
-  } else {
-    lo(occ_k(copy_kernel<16, 1>));
-    lo(occ_k(vx_kernel<16, 1>));
-  }
-  return m;
+int occupancy_copy(int n) {
+  if (n <= 2) return occ_k(copy_kernel<2, 8>);
+  if (n <= 4) return occ_k(copy_kernel<4, 4>);
+  if (n <= 8) return occ_k(copy_kernel<8, 2>);
+  return occ_k(copy_kernel<16, 1>);
+}
+int occupancy_vx(int n) {
+  if (n <= 2) return occ_k(vx_kernel<2, 8>);
+  if (n <= 4) return occ_k(vx_kernel<4, 4>);
+  if (n <= 8) return occ_k(vx_kernel<8, 2>);
+  return occ_k(vx_kernel<16, 1>);
 }
 
 }  // namespace mpigx

@@ -225,18 +225,26 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef MPIGX_NT_STORE
 #define MPIGX_NT_STORE 0  // fold outputs: plain stores measured >= nt (tools/local_tune.hip)
 #endif
+// Every streamed operand is HBM (ours or a peer's, IPC-mapped): accessed
+// through GLOBAL address-space pointers.  Through generic pointers the
+// compiler emits FLAT loads/stores, which count against lgkmcnt as well as
+// vmcnt and may alias LDS; in the kernels that stage their argument block
+// in LDS (fold/ar_zc/copy/scan) every re-read of a source pointer from LDS
+// then waited for all outstanding loads (s_waitcnt vmcnt(0) lgkmcnt(0)
+// between the loads of one thread: ~1 load in flight whatever the unroll).
+#define MPIGX_GPTR(T, p) ((__attribute__((address_space(1))) T*)(p))
 __device__ __forceinline__ u32x4 ld16(const void* p) {
 #if MPIGX_NT
-  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return __builtin_nontemporal_load(MPIGX_GPTR(const u32x4, p));
 #else
-  return *reinterpret_cast<const u32x4*>(p);
+  return *MPIGX_GPTR(const u32x4, p);
 #endif
 }
 __device__ __forceinline__ void st16(void* p, u32x4 v) {
 #if MPIGX_NT_STORE
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+  __builtin_nontemporal_store(v, MPIGX_GPTR(u32x4, p));
 #else
-  *reinterpret_cast<u32x4*>(p) = v;
+  *MPIGX_GPTR(u32x4, p) = v;
 #endif
 }
 
@@ -607,42 +615,88 @@ __device__ __forceinline__ void block_gather(char* const (&dst)[NMAX], const cha
 }
 
 // block_gather with UG 16-B vectors per pair per iteration: UG * m loads in
-// flight per thread before any store (ar_zc_kernel sizes UG so that a thread
-// keeps ~16 loads outstanding at any rank count; with one peer the plain
-// block_gather keeps ONE, which held the n = 2 allgather far below the HBM
-// rate).  Unaligned pairs fall back to block_gather.
-template <int NMAX, int UG>
-__device__ __forceinline__ void block_gather_u(char* const (&dst)[NMAX], const char* const (&src)[NMAX],
-                                               const long long (&len)[NMAX], int m) {
-  bool vec = true;
+// flight per thread before any store (ar_zc_kernel / copy_kernel size UG so
+// that a thread keeps ~16 loads outstanding at any rank count; with one peer
+// the plain block_gather keeps ONE).  The loads carry no guard at all — a
+// lane past the end of a shorter pair re-reads that pair's last vector, an
+// empty pair re-reads another pair's — and only the stores are guarded: any
+// branch between the loads (per-lane range guards, or even a wave-uniform
+// "pair p < m" test) made the compiler wait for the outstanding loads at the
+// join (vmcnt(0)), one or two loads in flight.  So the pair count is a
+// template parameter: block_gather_u dispatches m to block_gather_k<m>.
+// Unaligned pairs fall back to block_gather.
+template <int K, int UG, int MP>
+__device__ __forceinline__ void block_gather_k(char* const (&dst)[MP], const char* const (&src)[MP],
+                                               const long long (&len)[MP]) {
+  const long long tid = threadIdx.x, nt = blockDim.x;
   long long nvmax = 0;
+  int any = -1;
 #pragma unroll
-  for (int p = 0; p < NMAX; ++p)
-    if (p < m) {
-      vec &= ((((uintptr_t)dst[p]) | ((uintptr_t)src[p])) & 15) == 0;
-      const long long nv = len[p] / 16;
-      nvmax = nv > nvmax ? nv : nvmax;
+  for (int p = 0; p < K; ++p) {
+    const long long nv = len[p] / 16;
+    nvmax = nv > nvmax ? nv : nvmax;
+    if (nv > 0 && any < 0) any = p;
+  }
+  if (any < 0) return;
+  const char* s_any = src[0];
+  long long l_any = 0;
+#pragma unroll
+  for (int p = 0; p < K; ++p)
+    if (p == any) {
+      s_any = src[p];
+      l_any = len[p] / 16 - 1;
     }
+  const char* s[K];
+  long long last[K];
+#pragma unroll
+  for (int p = 0; p < K; ++p) {
+    const bool own = len[p] >= 16;
+    s[p] = own ? src[p] : s_any;
+    last[p] = own ? len[p] / 16 - 1 : l_any;
+  }
+  for (long long i = tid; i < nvmax; i += UG * nt) {
+    u32x4 v[K][UG];
+#pragma unroll
+    for (int p = 0; p < K; ++p)
+#pragma unroll
+      for (int u = 0; u < UG; ++u) {
+        const long long k = i + u * nt;
+        v[p][u] = ld16(s[p] + 16 * (k < last[p] ? k : last[p]));
+      }
+#pragma unroll
+    for (int p = 0; p < K; ++p)
+#pragma unroll
+      for (int u = 0; u < UG; ++u) {
+        const long long k = i + u * nt;
+        if (k < len[p] / 16) st16(dst[p] + 16 * k, v[p][u]);
+      }
+  }
+}
+
+template <int MP, int UG>
+__device__ __forceinline__ void block_gather_u(char* const (&dst)[MP], const char* const (&src)[MP],
+                                               const long long (&len)[MP], int m) {
+  bool vec = true;
+#pragma unroll
+  for (int p = 0; p < MP; ++p)
+    if (p < m) vec &= ((((uintptr_t)dst[p]) | ((uintptr_t)src[p])) & 15) == 0;
   if (!vec) {
-    block_gather<NMAX>(dst, src, len, m);
+    block_gather<MP>(dst, src, len, m);
     return;
   }
-  const long long tid = threadIdx.x, nt = blockDim.x;
-  for (long long i = tid; i < nvmax; i += UG * nt) {
-    u32x4 v[NMAX][UG];
-#pragma unroll
-    for (int p = 0; p < NMAX; ++p)
-#pragma unroll
-      for (int u = 0; u < UG; ++u)
-        if (p < m && i + u * nt < len[p] / 16) v[p][u] = ld16(src[p] + 16 * (i + u * nt));
-#pragma unroll
-    for (int p = 0; p < NMAX; ++p)
-#pragma unroll
-      for (int u = 0; u < UG; ++u)
-        if (p < m && i + u * nt < len[p] / 16) st16(dst[p] + 16 * (i + u * nt), v[p][u]);
+  switch (m) {  // wave-uniform
+#define MPIGX_GK(K) \
+  case K:           \
+    if constexpr (K <= MP) block_gather_k<K, UG, MP>(dst, src, len); \
+    break;
+    MPIGX_GK(1) MPIGX_GK(2) MPIGX_GK(3) MPIGX_GK(4) MPIGX_GK(5) MPIGX_GK(6) MPIGX_GK(7) MPIGX_GK(8)
+    MPIGX_GK(9) MPIGX_GK(10) MPIGX_GK(11) MPIGX_GK(12) MPIGX_GK(13) MPIGX_GK(14) MPIGX_GK(15) MPIGX_GK(16)
+#undef MPIGX_GK
+    default: break;
   }
+  const long long tid = threadIdx.x, nt = blockDim.x;
 #pragma unroll
-  for (int p = 0; p < NMAX; ++p)
+  for (int p = 0; p < MP; ++p)
     if (p < m)
       for (long long j = (len[p] / 16) * 16 + tid; j < len[p]; j += nt) dst[p][j] = src[p][j];
 }

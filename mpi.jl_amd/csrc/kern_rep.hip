@@ -95,26 +95,29 @@ hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs
 }
 
 // ar_zc_kernel instantiations (kernels.hpp): NMAX = n rounded up to a power
-// of two, U = 16 / NMAX; SH_FULL when every one of the NMAX leaves is present
-// with no pre-step, else SH_PRE.  nmax/shape come from arzc_shape (launch.hpp).
+// of two, U = 16 / NMAX vectors per thread scaled by the registers one vector
+// takes (zc_u, kernels.hpp: 8- and 16-bit elements hold one element per
+// VGPR); SH_FULL when every one of the NMAX leaves is present with no
+// pre-step, else SH_PRE.  nmax/shape come from arzc_shape (launch.hpp).
 template <class OP>
 hipError_t arzc_op(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a) {
   if (nmax == 2)
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 2, SH_FULL, 8>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 2, SH_FULL, zc_u<T>(8)>), grid, dim3(kThreads), 0, s, a);
   else if (nmax == 4 && shape == SH_FULL)
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_FULL, 4>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_FULL, zc_u<T>(4)>), grid, dim3(kThreads), 0, s, a);
   else if (nmax == 4)
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_PRE, 4>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_PRE, zc_u<T>(4)>), grid, dim3(kThreads), 0, s, a);
   else if (shape == SH_FULL)
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_FULL, 2>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_FULL, zc_u<T>(2)>), grid, dim3(kThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_PRE, 2>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_PRE, zc_u<T>(2)>), grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
-// Resident 256-thread blocks per CU of the kernels that spin on their peers
-// (fold / ring / scan / ar_zc) for an nmax (8: n <= 8, 16: n <= 16): the
-// smallest over the instantiations a communicator of that size can launch.
+// Resident 256-thread blocks per CU of ONE kernel that spins on its peers
+// (the host caps that launch's grid with it, mpigx.cpp kernel_cap).
+//   kind 0 fold_kernel (a = nmax, b = sched), 1 ar_zc_kernel (a = nmax,
+//   b = shape), 2 ring_kernel, 3 scan_kernel
 template <class K>
 int occ1(K k) {
   int nb = 0;
@@ -125,24 +128,20 @@ int occ1(K k) {
   return nb;
 }
 template <class OP>
-int occ_op(int nmax) {
-  int m = 1 << 20;
-  auto lo = [&](int v) { m = v < m ? v : m; };
-  if (nmax <= 8) {
-    lo(occ1(fold_kernel<OP, T, 8, S_TREE>));
-    lo(occ1(fold_kernel<OP, T, 8, S_LINEAR>));
-    lo(occ1(ar_zc_kernel<OP, T, 2, SH_FULL, 8>));
-    lo(occ1(ar_zc_kernel<OP, T, 4, SH_FULL, 4>));
-    lo(occ1(ar_zc_kernel<OP, T, 4, SH_PRE, 4>));
-    lo(occ1(ar_zc_kernel<OP, T, 8, SH_FULL, 2>));
-    lo(occ1(ar_zc_kernel<OP, T, 8, SH_PRE, 2>));
-  } else {
-    lo(occ1(fold_kernel<OP, T, 16, S_TREE>));
-    lo(occ1(fold_kernel<OP, T, 16, S_LINEAR>));
+int occ_op(int kind, int a, int b) {
+  switch (kind) {
+    case 0:
+      if (a <= 8) return b == S_LINEAR ? occ1(fold_kernel<OP, T, 8, S_LINEAR>) : occ1(fold_kernel<OP, T, 8, S_TREE>);
+      return b == S_LINEAR ? occ1(fold_kernel<OP, T, 16, S_LINEAR>) : occ1(fold_kernel<OP, T, 16, S_TREE>);
+    case 1:
+      if (a == 2) return occ1(ar_zc_kernel<OP, T, 2, SH_FULL, zc_u<T>(8)>);
+      if (a == 4) return b == SH_FULL ? occ1(ar_zc_kernel<OP, T, 4, SH_FULL, zc_u<T>(4)>)
+                                      : occ1(ar_zc_kernel<OP, T, 4, SH_PRE, zc_u<T>(4)>);
+      return b == SH_FULL ? occ1(ar_zc_kernel<OP, T, 8, SH_FULL, zc_u<T>(2)>)
+                          : occ1(ar_zc_kernel<OP, T, 8, SH_PRE, zc_u<T>(2)>);
+    case 2: return occ1(ring_kernel<OP, T>);
+    default: return occ1(scan_kernel<OP, T>);
   }
-  lo(occ1(ring_kernel<OP, T>));
-  lo(occ1(scan_kernel<OP, T>));
-  return m;
 }
 }  // namespace
 
@@ -152,7 +151,7 @@ int occ_op(int nmax) {
 #define MPIGX_OCC_FN(K) MPIGX_CAT4(occupancy_, MPIGX_REP_NAME, _o, K)
 #define MPIGX_DECL_OP(K)                                                                               \
   hipError_t MPIGX_ARZC_FN(K)(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a);      \
-  int MPIGX_OCC_FN(K)(int nmax);                                                                       \
+  int MPIGX_OCC_FN(K)(int kind, int a, int b);                                                         \
   hipError_t MPIGX_FOLD_FN(K)(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a);      \
   hipError_t MPIGX_RING_FN(K)(dim3 grid, hipStream_t s, const RingArgs& a);                            \
   hipError_t MPIGX_SCAN_FN(K)(dim3 grid, hipStream_t s, const ScanArgs& a);                            \
@@ -171,9 +170,9 @@ MPIGX_DECL_OP(6) MPIGX_DECL_OP(7) MPIGX_DECL_OP(8) MPIGX_DECL_OP(9) MPIGX_DECL_O
     if constexpr (valid_op(K)) return arzc_op<OpOf<K>::type>(nmax, shape, grid, s, a);                 \
     return hipErrorInvalidValue;                                                                       \
   }                                                                                                    \
-  int MPIGX_OCC_FN(K)(int nmax) {                                                                      \
-    if constexpr (valid_op(K)) return occ_op<OpOf<K>::type>(nmax);                                     \
-    return 1 << 20;                                                                                    \
+  int MPIGX_OCC_FN(K)(int kind, int a, int b) {                                                        \
+    if constexpr (valid_op(K)) return occ_op<OpOf<K>::type>(kind, a, b);                               \
+    return 0;                                                                                          \
   }                                                                                                    \
   hipError_t MPIGX_RING_FN(K)(dim3 grid, hipStream_t s, const RingArgs& a) {                           \
     if constexpr (valid_op(K)) {                                                                       \
@@ -257,24 +256,20 @@ hipError_t MPIGX_CAT(launch_arzc_, MPIGX_REP_NAME)(int op, int nmax, int shape, 
                                                   const FoldArgs& a) {
   MPIGX_SWITCH(MPIGX_ARZC_FN, nmax, shape, grid, s, a)
 }
-int MPIGX_CAT(occupancy_, MPIGX_REP_NAME)(int nmax) {
-  int m = 1 << 20;
-  auto lo = [&](int v) { m = v < m ? v : m; };
-  lo(MPIGX_OCC_FN(0)(nmax));
-  lo(MPIGX_OCC_FN(1)(nmax));
-  if constexpr (!kCplx) {
-    lo(MPIGX_OCC_FN(2)(nmax));
-    lo(MPIGX_OCC_FN(3)(nmax));
-    lo(MPIGX_OCC_FN(4)(nmax));
-    lo(MPIGX_OCC_FN(5)(nmax));
-    lo(MPIGX_OCC_FN(6)(nmax));
+int MPIGX_CAT(occupancy_, MPIGX_REP_NAME)(int op, int kind, int a, int b) {
+  switch (op) {
+    case O_SUM: return MPIGX_OCC_FN(0)(kind, a, b);
+    case O_PROD: return MPIGX_OCC_FN(1)(kind, a, b);
+    case O_MIN: return MPIGX_OCC_FN(2)(kind, a, b);
+    case O_MAX: return MPIGX_OCC_FN(3)(kind, a, b);
+    case O_LAND: return MPIGX_OCC_FN(4)(kind, a, b);
+    case O_LOR: return MPIGX_OCC_FN(5)(kind, a, b);
+    case O_LXOR: return MPIGX_OCC_FN(6)(kind, a, b);
+    case O_BAND: return MPIGX_OCC_FN(7)(kind, a, b);
+    case O_BOR: return MPIGX_OCC_FN(8)(kind, a, b);
+    case O_BXOR: return MPIGX_OCC_FN(9)(kind, a, b);
+    default: return 0;
   }
-  if constexpr (kInt) {
-    lo(MPIGX_OCC_FN(7)(nmax));
-    lo(MPIGX_OCC_FN(8)(nmax));
-    lo(MPIGX_OCC_FN(9)(nmax));
-  }
-  return m;
 }
 hipError_t MPIGX_CAT(launch_ring_, MPIGX_REP_NAME)(int op, dim3 grid, hipStream_t s, const RingArgs& a) {
   MPIGX_SWITCH(MPIGX_RING_FN, grid, s, a)

@@ -43,6 +43,20 @@ __device__ __forceinline__ void signal_done(const PeerView& pv, int aborted = 0)
   }
 }
 
+// Vectors per thread in flight for the collective folds: U 16-B vectors of
+// 4-byte-or-wider elements, fewer where one vector takes more than 4 VGPRs
+// (8- / 16-bit elements sit one per VGPR: 16 / 8 registers per vector), so
+// the int8 kernels do not trade occupancy for loads they cannot hold.
+template <class T>
+constexpr int vec_regs() {
+  using V = Vec<T, VecW<T>::v>;
+  return V::N * (sizeof(typename V::S) >= 4 ? (int)(sizeof(typename V::S) / 4) : 1);
+}
+template <class T>
+constexpr int zc_u(int U) {
+  return U * 4 / vec_regs<T>() >= 1 ? U * 4 / vec_regs<T>() : 1;
+}
+
 template <class OP, class T, int NMAX, int SCHED>
 __device__ __forceinline__ int fold_body(const FoldArgs& A);
 
@@ -137,7 +151,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
   // two vectors per thread in flight in every fold and gather of the
   // collective modes at n <= 8 (ar_zc_kernel goes further for the headline
   // zero-copy two-shot); NMAX 16 (n = 9..16) keeps one (VGPRs)
-  constexpr int FU = NMAX <= 8 ? 2 : 1;
+  constexpr int FU = NMAX <= 8 ? zc_u<T>(2) : 1;
   const T* const* src = reinterpret_cast<const T* const*>(A.src);
   const T* const* src2 = reinterpret_cast<const T* const*>(A.src2);
   const PeerView& pv = A.pv;
@@ -531,11 +545,12 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
   }
   stamp(pv, 3);
   if (!ab) {
-    char* dsts[NMAX];
-    const char* srcs[NMAX];
-    long long lens[NMAX];
+    constexpr int MP = NMAX - 1;  // peers: n - 1 <= NMAX - 1
+    char* dsts[MP];
+    const char* srcs[MP];
+    long long lens[MP];
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j) {
+    for (int j = 0; j < MP; ++j) {
       dsts[j] = nullptr;
       srcs[j] = nullptr;
       lens[j] = 0;
@@ -548,7 +563,7 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
         lens[j] = (h2 - l2) * es;
       }
     }
-    block_gather_u<NMAX, U>(dsts, srcs, lens, n - 1);
+    block_gather_u<MP, U>(dsts, srcs, lens, n - 1);
   }
   stamp(pv, 4);
   rank_barrier(pv, ep++, &ab);  // nobody reads my buffers any more

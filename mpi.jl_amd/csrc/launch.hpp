@@ -14,7 +14,9 @@ using ScanLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const Scan
 using RingLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const RingArgs& a);
 
 using ArzcLauncher = hipError_t (*)(int op, int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a);
-using OccQuery = int (*)(int nmax);
+// resident blocks per CU of one spinning kernel: (op, kind 0 fold / 1 ar_zc /
+// 2 ring / 3 scan, a, b) — kern_rep.hip occ_op
+using OccQuery = int (*)(int op, int kind, int a, int b);
 
 // ar_zc_kernel (kernels.hpp) instantiation for a communicator of n <= 8
 // ranks and the planned fold (ntree leaves, rem pre-step pairs): NMAX = n
@@ -29,7 +31,7 @@ inline bool arzc_shape(int n, int ntree, int rem, int* nmax, int* shape) {
 
 #define MPIGX_DECL_REP(NAME)                                                                     \
   hipError_t launch_arzc_##NAME(int op, int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a); \
-  int occupancy_##NAME(int nmax); \
+  int occupancy_##NAME(int op, int kind, int a, int b); \
   hipError_t launch_fold_##NAME(int op, int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a); \
   hipError_t launch_scan_##NAME(int op, dim3 grid, hipStream_t s, const ScanArgs& a); \
   hipError_t launch_ring_##NAME(int op, dim3 grid, hipStream_t s, const RingArgs& a); \
@@ -41,7 +43,8 @@ MPIGX_DECL_REP(bf16)
 #undef MPIGX_DECL_REP
 
 hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a);
-int occupancy_copy(int nmax);
+int occupancy_copy(int n);  // copy_kernel of an n-rank communicator
+int occupancy_vx(int n);    // vx_kernel likewise
 hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a);
 hipError_t launch_xfer(hipStream_t s, const XferArgs& a);
 hipError_t launch_pack(hipStream_t s, const PackArgs& a);

@@ -160,22 +160,28 @@ ArzcLauncher arzc_launcher(Rep r) {
     default: return nullptr;
   }
 }
-// Resident 256-thread blocks per CU of every kernel that spins on its peers
-// (all types and ops, the instantiations of this nmax): the grid cap's
-// occupancy (comm_init).  Queried once per process and nmax.
-int spin_occupancy(int nmax) {
-  static int cached[2] = {-1, -1};
-  int& v = cached[nmax > 8 ? 1 : 0];
-  if (v >= 0) return v;
-  const OccQuery qs[] = {occupancy_i8,  occupancy_u8,  occupancy_i16, occupancy_u16, occupancy_i32,
-                         occupancy_u32, occupancy_i64, occupancy_u64, occupancy_f32, occupancy_f64,
-                         occupancy_c64, occupancy_c128, occupancy_bf16};
-  int m = occupancy_copy(nmax);
-  for (OccQuery q : qs) {
-    const int o = q(nmax);
-    m = o < m ? o : m;
-  }
-  v = m;
+// Resident 256-thread blocks per CU of ONE kernel that spins on its peers
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor; process-wide cache): kind
+// 0 fold_kernel (a = nmax, b = sched), 1 ar_zc_kernel (a = nmax, b = shape),
+// 2 ring_kernel, 3 scan_kernel (kern_rep.hip occ_op), 10 copy_kernel and
+// 11 vx_kernel of an a-rank communicator (copy.hip).
+enum OccKind { OK_FOLD = 0, OK_ARZC = 1, OK_RING = 2, OK_SCAN = 3, OK_COPY = 10, OK_VX = 11 };
+int kernel_occ(int rep, int op, int kind, int a, int b) {
+  static std::mutex mu;
+  static std::vector<std::pair<unsigned long long, int>> cache;
+  const unsigned long long key = ((unsigned long long)(rep + 1) << 40) | ((unsigned long long)(op + 1) << 32) |
+                                 ((unsigned long long)kind << 16) | ((unsigned long long)a << 8) | (unsigned)b;
+  std::lock_guard<std::mutex> g(mu);
+  for (auto& e : cache)
+    if (e.first == key) return e.second;
+  static const OccQuery qs[R_COUNT] = {occupancy_i8,  occupancy_u8,  occupancy_i16, occupancy_u16, occupancy_i32,
+                                       occupancy_u32, occupancy_i64, occupancy_u64, occupancy_f32, occupancy_f64,
+                                       occupancy_c64, occupancy_c128, occupancy_bf16};
+  int v = 0;
+  if (kind == OK_COPY) v = occupancy_copy(a);
+  else if (kind == OK_VX) v = occupancy_vx(a);
+  else if (rep >= 0 && rep < R_COUNT) v = qs[rep](op, kind, a, b);
+  cache.push_back({key, v});
   return v;
 }
 ScanLauncher scan_launcher(Rep r) {
@@ -325,10 +331,34 @@ int finish(mpigx_comm* c) {
   return MPIGX_SUCCESS;
 }
 
-int grid_for(mpigx_comm* c, long long bytes) {
+// Grid cap of a kernel whose blocks spin on their peers: every rank's grid
+// must be resident at once, so at most CUs x (resident blocks per CU of THAT
+// kernel) / (ranks sharing the most-loaded device).  The occupancy API can
+// admit one block per CU more than the hardware where SGPRs bind (>= 6 blocks
+// of 256 threads, MI355X_MICROARCH.md "Residency"): one fewer there;
+// VGPR-bound counts (<= 5) are exact.  The same on every rank (same kernel,
+// agreed cus_min / dev_share).
+int kernel_cap(mpigx_comm* c, int occ) {
+  const long long o = occ >= 6 ? occ - 1 : occ > 0 ? occ : 1;
+  const long long cap = (long long)c->cus_min * o / (c->dev_share > 0 ? c->dev_share : 1);
+  return (int)(cap < 1 ? 1 : cap > kMaxBlocks ? kMaxBlocks : cap);
+}
+int cap_fold(mpigx_comm* c, const TypeInfo* t, int oc, int nmax, int sched) {
+  return kernel_cap(c, kernel_occ(t->rep, oc, OK_FOLD, nmax, sched));
+}
+int cap_arzc(mpigx_comm* c, const TypeInfo* t, int oc, int nmax, int shape) {
+  return kernel_cap(c, kernel_occ(t->rep, oc, OK_ARZC, nmax, shape));
+}
+int cap_ring(mpigx_comm* c, const TypeInfo* t, int oc) { return kernel_cap(c, kernel_occ(t->rep, oc, OK_RING, 0, 0)); }
+int cap_scan(mpigx_comm* c, const TypeInfo* t, int oc) { return kernel_cap(c, kernel_occ(t->rep, oc, OK_SCAN, 0, 0)); }
+int cap_copy(mpigx_comm* c) { return kernel_cap(c, kernel_occ(-1, -1, OK_COPY, c->n, 0)); }
+int cap_vx(mpigx_comm* c) { return kernel_cap(c, kernel_occ(-1, -1, OK_VX, c->n, 0)); }
+
+int grid_for(mpigx_comm* c, long long bytes, int cap) {
   long long g = cdiv(bytes, c->bytes_per_block);
   if (g < 1) g = 1;
   if (g > c->max_blocks) g = c->max_blocks;
+  if (g > cap) g = cap;
   return (int)g;
 }
 
@@ -679,12 +709,15 @@ int allreduce_zc(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeIn
   for (int p = 0; p < n; ++p) ptrs[p] = z.ps[p];
   plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
   a.chunk = rup(cdiv(count, n), vec);
-  const int grid = grid_for(c, a.chunk * es);
-  a.slice = rup(cdiv(a.chunk, grid), vec);
   // the dedicated kernel (kernels.hpp ar_zc_kernel) for the MPICH tree at
   // n <= 8; the all-modes fold_kernel for LINEAR order and n > 8 (same bits)
   int znmax, zshape;
-  if (sched == S_TREE && c->algo != MPIGX_ALGO_PULL_GENERIC && arzc_shape(n, a.ntree, a.rem, &znmax, &zshape))
+  const bool dedicated =
+      sched == S_TREE && c->algo != MPIGX_ALGO_PULL_GENERIC && arzc_shape(n, a.ntree, a.rem, &znmax, &zshape);
+  const int grid = grid_for(c, a.chunk * es, dedicated ? cap_arzc(c, t, oc, znmax, zshape)
+                                                        : cap_fold(c, t, oc, nmax, sched));
+  a.slice = rup(cdiv(a.chunk, grid), vec);
+  if (dedicated)
     HIPCK(arzc_launcher(t->rep)(oc, znmax, zshape, dim3(grid), c->stream, a));
   else
     HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
@@ -736,7 +769,7 @@ int allreduce_push(mpigx_comm* c, const ZcLaunch& z, const void* send, long long
       ptrs[q] = q == r ? (const void*)a.send : (const void*)(c->stage + (long long)q * a.slot_bytes - c0 * es);
     int nmax, sched;
     plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
-    const int grid = grid_for(c, a.chunk * es);
+    const int grid = grid_for(c, a.chunk * es, cap_fold(c, t, oc, nmax, sched));
     a.slice = rup(cdiv(a.chunk, grid), vec);
     HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
     note_launch(c, a.pv, grid);
@@ -796,8 +829,11 @@ int allreduce_ring(mpigx_comm* c, const ZcLaunch& z, long long count, const Type
     a.count = cnt;
     a.part = rup(cdiv(cnt, nch), (long long)n * vec);
     a.chunk = a.part / n;
-    int gc = grid_for(c, a.chunk * es);
-    if (gc * nch > c->max_blocks) gc = c->max_blocks / nch > 0 ? c->max_blocks / nch : 1;
+    // nch rings share the grid: the whole grid within MAX_BLOCKS and the cap
+    const int rcap = cap_ring(c, t, oc);
+    int gc = grid_for(c, a.chunk * es, rcap);
+    const int lim = c->max_blocks < rcap ? c->max_blocks : rcap;
+    if (gc * nch > lim) gc = lim / nch > 0 ? lim / nch : 1;
     a.slice = rup(cdiv(a.chunk, gc), vec);
     for (int q = 0; q < n; ++q) {
       a.zsend[q] = z.ps[q] ? z.ps[q] + off * es : nullptr;
@@ -1067,7 +1103,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
         for (int p = 0; p < n; ++p) ptrs[p] = z.ps[p] ? z.ps[p] + off * es : nullptr;
         plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
         a.chunk = rup(cdiv(cnt, n), vec);
-        const int grid = grid_for(c, a.chunk * es);
+        const int grid = grid_for(c, a.chunk * es, cap_fold(c, t, oc, nmax, sched));
         a.slice = rup(cdiv(a.chunk, grid), vec);
         HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
         note_launch(c, a.pv, grid);
@@ -1105,7 +1141,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     for (int q = 0; q < n; ++q)
       ptrs[q] = q == c->rank ? send : (const void*)(c->stage + q * ustride - c0 * es);
     plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
-    const int grid = grid_for(c, a.chunk * es);
+    const int grid = grid_for(c, a.chunk * es, cap_fold(c, t, oc, nmax, sched));
     a.slice = rup(cdiv(a.chunk, grid), vec);
     HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
     note_launch(c, a.pv, grid);
@@ -1131,7 +1167,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     const void* ptrs[kMaxRanks];
     for (int p = 0; p < n; ++p) ptrs[p] = c->stage + p * ustride;
     plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
-    const int grid = grid_for(c, count * es);
+    const int grid = grid_for(c, count * es, cap_fold(c, t, oc, nmax, sched));
     a.slice = rup(cdiv(count, grid), vec);
     HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
     note_launch(c, a.pv, grid);
@@ -1160,13 +1196,13 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     int grid, nbar;
     if (oneshot) {
       a.mode = all ? M_AR_ONESHOT : M_RED_ONESHOT;
-      grid = grid_for(c, cnt * es);
+      grid = grid_for(c, cnt * es, cap_fold(c, t, oc, nmax, sched));
       a.slice = rup(cdiv(cnt, grid), vec);
       nbar = 2;
     } else {
       a.mode = all ? M_AR_TWOSHOT : M_RED_TWOSHOT;
       a.chunk = rup(cdiv(cnt, n), vec);
-      grid = grid_for(c, a.chunk * es);
+      grid = grid_for(c, a.chunk * es, cap_fold(c, t, oc, nmax, sched));
       a.slice = rup(cdiv(a.chunk, grid), vec);
       nbar = 3;
     }
@@ -1280,7 +1316,7 @@ int vexchange(mpigx_comm* c, const VSpec& s) {
   const long long R = ((long long)(c->stage_bytes - kSlotBase) / n) & ~15ll;
   if (R < 16) return MPIGX_ERR_NO_MEM;
   const long long per_round = gmax < R ? gmax : R;
-  const int G = grid_for(c, per_round * n);
+  const int G = grid_for(c, per_round * n, cap_vx(c));
   for (long long off = 0; off < gmax; off += R) {
     VArgs a;
     memset(&a, 0, sizeof a);
@@ -1494,7 +1530,7 @@ int knob_apply(mpigx_comm* c, int k, long long v, bool init) {
       return MPIGX_SUCCESS;
     case MPIGX_KNOB_MAX_BLOCKS: {
       if (!in(1, kMaxBlocks)) return MPIGX_ERR_ARG;
-      c->max_blocks = (int)(v < c->max_blocks_cap ? v : c->max_blocks_cap);
+      c->max_blocks = (int)v;
       return MPIGX_SUCCESS;
     }
     case MPIGX_KNOB_ONESHOT_MAX:
@@ -1677,6 +1713,12 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   c->peer_stage[rank] = c->stage;
   c->peer_sig[rank] = c->sig;
   c->peer_ll[rank] = c->ll;
+  {
+    int cus = 0;
+    HIPCK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    c->cus_min = cus > 0 ? cus : 1;
+    c->dev_share = 1;
+  }
   if (nranks == 1) return MPIGX_SUCCESS;
 
   // rendezvous
@@ -1728,7 +1770,6 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   me.pci_dev = prop.pciDeviceID;
   me.pci_domain = prop.pciDomainID;
   me.cus = prop.multiProcessorCount;
-  me.occupancy = spin_occupancy(nranks <= 8 ? 8 : 16);
   for (int k = 0; k < MPIGX_KNOB_COUNT; ++k) me.knobs[k] = knob_value(c, k);
   me.epoch0 = c->epoch;
   me.stage_bytes = c->stage_bytes;
@@ -1757,10 +1798,10 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
     if (pr.epoch0 != me.epoch0) return MPIGX_ERR_ARG;  // MPIGX_EPOCH_BASE likewise
   }
   // ranks sharing a device: every rank's grid of a spinning kernel must be
-  // resident at once (include/mpigx.h mpigx_comm_device_share)
+  // resident at once (kernel_cap: per launched kernel, from cus_min and
+  // dev_share; include/mpigx.h mpigx_comm_device_share)
   {
-    int share = 1;
-    long long cap = kMaxBlocks;
+    int share = 1, cus = me.cus;
     for (int q = 0; q < nranks; ++q) {
       const ShmRank& a = c->shm->ranks[q];
       int k = 0;
@@ -1769,16 +1810,10 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
         k += b.pci_domain == a.pci_domain && b.pci_bus == a.pci_bus && b.pci_dev == a.pci_dev;
       }
       share = k > share ? k : share;
-      // the occupancy API can admit one block per CU more than the hardware
-      // where SGPRs bind (>= 6 blocks of 256 threads, MI355X_MICROARCH.md
-      // "Residency"): one fewer there; VGPR-bound counts (<= 5) are exact
-      const long long occ = a.occupancy >= 6 ? a.occupancy - 1 : a.occupancy > 0 ? a.occupancy : 1;
-      const long long cq = (long long)a.cus * occ / k;
-      cap = cq < cap ? cq : cap;
+      cus = a.cus < cus ? a.cus : cus;
     }
     c->dev_share = share;
-    c->max_blocks_cap = (int)(cap < 1 ? 1 : cap);
-    if (c->max_blocks > c->max_blocks_cap) c->max_blocks = c->max_blocks_cap;
+    c->cus_min = cus;
     const long long limit_share = env_ll("MPIGX_MAX_RANKS_PER_DEVICE", 10);
     if (share > limit_share) {
       fprintf(stderr,
@@ -2016,7 +2051,7 @@ int mpigx_comm_get_knob(mpigx_comm_t c, int knob, long long* value) {
 int mpigx_comm_device_share(mpigx_comm_t c, int* ranks, int* cap) {
   if (!c) return MPIGX_ERR_COMM;
   if (ranks) *ranks = c->dev_share;
-  if (cap) *cap = c->max_blocks_cap;
+  if (cap) *cap = c->cus_min / (c->dev_share > 0 ? c->dev_share : 1);
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_set_stamps(mpigx_comm_t c, void* stamps) {
@@ -2051,7 +2086,7 @@ int mpigx_comm_probe(mpigx_comm_t c, int kind, long long bytes, double* seconds)
   a.pv = make_view(c);
   a.mode = kind == 1 ? C_PROBE_ONE : C_PROBE_ALL;
   a.bytes = bytes;
-  const int g = c->max_blocks;
+  const int g = c->max_blocks < cap_copy(c) ? c->max_blocks : cap_copy(c);
   a.slice = rup(cdiv(bytes, g), 16);
   hipEvent_t e0, e1;
   HIPCK(hipEventCreate(&e0));
@@ -2106,7 +2141,7 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
     a.send = buf;
     a.recv = buf;
     if (int e = ll_fill(c, a.pv, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
-    const int g = grid_for(c, bytes);
+    const int g = grid_for(c, bytes, cap_copy(c));
     a.slice = rup(cdiv(bytes, g), 16);
     HIPCK(launch_copy(dim3(g), c->stream, a));
     note_launch(c, a.pv, g);
@@ -2130,11 +2165,11 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
       if (sag) {
         a.mode = C_BCAST_SAG_ZC;
         a.chunk = rup(cdiv(bytes, c->n), 16);
-        g = grid_for(c, a.chunk);
+        g = grid_for(c, a.chunk, cap_copy(c));
         a.slice = rup(cdiv(a.chunk, g), 16);
       } else {
         a.mode = C_BCAST_ZC;
-        g = grid_for(c, bytes);
+        g = grid_for(c, bytes, cap_copy(c));
         a.slice = rup(cdiv(bytes, g), 16);
       }
       HIPCK(launch_copy(dim3(g), c->stream, a));
@@ -2158,11 +2193,11 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
     if (sag) {
       a.mode = C_BCAST_SAG;
       a.chunk = rup(cdiv(len, c->n), 16);
-      g = grid_for(c, a.chunk);
+      g = grid_for(c, a.chunk, cap_copy(c));
       a.slice = rup(cdiv(a.chunk, g), 16);
     } else {
       a.mode = C_BCAST;
-      g = grid_for(c, len);
+      g = grid_for(c, len, cap_copy(c));
       a.slice = rup(cdiv(len, g), 16);
     }
     HIPCK(launch_copy(dim3(g), c->stream, a));
@@ -2210,7 +2245,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
     a.send = s;
     a.recv = recv;
     if (int e = ll_fill(c, a.pv, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
-    const int g = grid_for(c, bytes);
+    const int g = grid_for(c, bytes, cap_copy(c));
     a.slice = rup(cdiv(bytes, g), 16);
     HIPCK(launch_copy(dim3(g), c->stream, a));
     note_launch(c, a.pv, g);
@@ -2231,7 +2266,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
       a.bytes = bytes;
       a.total = bytes;
       for (int p = 0; p < n; ++p) a.zsrc[p] = z.ps[p];
-      const int g = grid_for(c, bytes * n);
+      const int g = grid_for(c, bytes * n, cap_copy(c));
       a.slice = rup(cdiv(bytes, g), 16);
       a.send = s;
       a.recv = recv;
@@ -2256,7 +2291,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
       a.bytes = bytes;
       a.total = bytes;
       for (int p = 0; p < n; ++p) a.zsrc[p] = z.ps[p];
-      const int g = grid_for(c, bytes);
+      const int g = grid_for(c, bytes, cap_copy(c));
       a.slice = rup(cdiv(bytes, g), 16);
       a.send = s;
       a.recv = recv;
@@ -2279,7 +2314,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
     a.bytes = len;
     a.total = bytes;
     a.sstride = rup(len, 16);
-    const int g = grid_for(c, len * (alltoall ? n : 1));
+    const int g = grid_for(c, len * (alltoall ? n : 1), cap_copy(c));
     a.slice = rup(cdiv(len, g), 16);
     if (alltoall) {
       a.send = s + off;
@@ -2885,7 +2920,7 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
       a.exclusive = exclusive;
       a.esize = es;
       a.count = count;
-      const int g = grid_for(c, (long long)count * es);
+      const int g = grid_for(c, (long long)count * es, cap_scan(c, t, oc));
       a.slice = rup(cdiv(count, g), vec);
       a.send = s;
       a.recv = recvbuf;
@@ -2908,7 +2943,7 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
     a.exclusive = exclusive;
     a.esize = es;
     a.count = count;
-    const int g = grid_for(c, (long long)count * es);
+    const int g = grid_for(c, (long long)count * es, cap_scan(c, t, oc));
     a.slice = rup(cdiv(count, g), vec);
     a.send = s;
     a.recv = recvbuf;
@@ -2930,7 +2965,7 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
     a.exclusive = exclusive;
     a.esize = es;
     a.count = cnt;
-    const int g = grid_for(c, cnt * es);
+    const int g = grid_for(c, cnt * es, cap_scan(c, t, oc));
     a.slice = rup(cdiv(cnt, g), vec);
     a.send = (const char*)s + off * es;
     a.recv = (char*)recvbuf + off * es;

@@ -23,9 +23,7 @@ struct ShmRank {
   int pci_bus;
   int pci_dev;
   int pci_domain;
-  int occupancy;                 // resident blocks per CU of the spinning kernels (0: unknown)
   int cus;                       // compute units of my device
-  int pad;
   long long knobs[MPIGX_KNOB_COUNT];  // path-selecting settings read at init (must agree)
   unsigned long long epoch0;          // first barrier epoch (MPIGX_EPOCH_BASE; must agree)
   unsigned long long stage_bytes;
@@ -227,8 +225,8 @@ struct mpigx_comm {
   // tuning (the path-selecting knobs, include/mpigx.h MPIGX_KNOB_*: read once
   // at init, checked to agree on every rank, changed only collectively)
   int max_blocks = 256;
-  int max_blocks_cap = mpigx::kMaxBlocks;  // residency cap (ranks sharing a device)
-  int dev_share = 1;                       // ranks on the most-loaded device
+  int cus_min = 256;                       // compute units of the smallest device (agreed at init)
+  int dev_share = 1;                       // ranks on the most-loaded device (grid caps: kernel_cap)
   long long oneshot_max = 256 << 10;
   long long bcast_sag_min = 256 << 10;  // Bcast: scatter+allgather from this size (n >= 3)
   long long bytes_per_block = 64 << 10;

@@ -52,7 +52,7 @@ def extra(comm, r, n, f32_input, fails):
                 recv.zero_()
                 MPI.Allreduce_(xs[r], recv, MPI.SUM, comm)
                 got = recv.cpu().numpy()
-                if algo == "ring":
+                if algo == "ring" and count * 4 >= MPI.get_knob(comm, "ZC_MIN"):  # the ring is a zero-copy-size path
                     stage = MPI.get_knob(comm, "STAGING_BYTES")
                     exp = M.fold_ring(hs, "FLOAT", "SUM", 1, M.ring_round_elems(stage, n, "FLOAT", 1))
                 else:

@@ -112,6 +112,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--timeout", type=int, default=150)
     a = ap.parse_args()
+    a.out = os.path.abspath(a.out)  # the ranks (and rocprofv3's -d) run with cwd /tmp
     os.makedirs(a.out, exist_ok=True)
     summary = {"n": a.n, "tag": a.tag, "configs": {}}
     pmc_set = set(a.pmc_configs.split(",")) if a.pmc_configs else set()
