@@ -12,10 +12,10 @@ Per config (MiB:algo) three passes, each a fresh set of rank processes:
           ranks unprofiled;
   write : the same with WRITE_SIZE (FETCH_SIZE and WRITE_SIZE do not fit one
           TCC pass).
-The counters are the device's: with every rank on one GPU, rank 0's dispatch
-window also holds its peers' concurrent kernels, so FETCH/WRITE count the
-traffic of ALL ranks of that call (the algorithmic bytes below are counted
-the same way).  gfx950: FETCH_SIZE reports half the bytes of a 16-B/lane
+Measured (r03): the counters cover the profiled process's own dispatches
+only (rank 0's kernel: 2.50 S for a pull two-shot of S bytes at n = 2, which
+is one rank's algorithmic traffic), so traffic is compared with ONE rank's
+algorithmic bytes (all-rank bytes / n).  gfx950: FETCH_SIZE reports half the bytes of a 16-B/lane
 streaming read (MI355X_MICROARCH.md §HBM), so bytes = 2 * FETCH + WRITE.
 Writes <out_dir>/<config>_<pass>/..., and <out_dir>/<tag>_coll_summary.json.
 """
@@ -144,7 +144,7 @@ def main():
                     b = 2 * v["FETCH_SIZE_KB_median"] * 1024 + v["WRITE_SIZE_KB_median"] * 1024
                     v["hbm_bytes_device"] = b
                     v["algorithmic_bytes_all_ranks"] = algo_bytes(algo, a.n, S)
-                    v["traffic_over_algorithmic"] = round(b / algo_bytes(algo, a.n, S), 4)
+                    v["traffic_over_algorithmic_per_rank"] = round(b * a.n / algo_bytes(algo, a.n, S), 4)
             rec["traffic"] = tr
         dev_s = res["device_ms_median"] / 1e3
         rec["hbm_GBps_algorithmic"] = round(algo_bytes(algo, a.n, S) / dev_s / 1e9, 1)
