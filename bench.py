@@ -114,17 +114,19 @@ def cpu_reference_allreduce(ranks=8, mib=256, iters=3):
 
 
 def traffic_from_profiles(key):
-    """Per-launch HBM bytes from the committed PMC pass (profiles/*_traffic.json)."""
+    """(per-launch HBM bytes, file) from the newest committed PMC pass
+    (profiles/r<NN>*_traffic.json, tools/profile.sh: rocprofv3 cannot run
+    inside the process it profiles)."""
     import glob
-    best = None
+    best, src = None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
         try:
             j = json.load(open(f))
         except Exception:
             continue
         if key in j:
-            best = j[key]
-    return best
+            best, src = j[key], os.path.relpath(f, ROOT)
+    return best, src
 
 
 def bench_local(args):
@@ -212,7 +214,7 @@ def bench_local(args):
 
     achieved = algo / (kern_ms / 1e3) / 1e9
     value = algo / wall / 1e9
-    traffic = traffic_from_profiles("reduce_local_multi_f32_sum_8x256MiB")
+    traffic, traffic_src = traffic_from_profiles("reduce_local_multi_f32_sum_8x256MiB")
     res = {
         "metric": "Allreduce! busbw GB/s (256MiB f32 SUM) at 1/2/4/8 GPUs; % of xGMI/HBM peak",
         "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -227,7 +229,7 @@ def bench_local(args):
                      "kernel": "fold_local_kernel<OpSum,float,NMAX 8,TREE,SH_FULL,U 4>", "kernel_ms": round(kern_ms, 4),
                      "achieved_basis": "9 x 256 MiB algorithmic bytes / (HIP-event time over the K timed launches on the launch stream / K)",
                      "traffic_basis": "rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE per dispatch (gfx950 FETCH_SIZE "
-                                      "halving, MI355X_MICROARCH.md), profiles/r02_traffic.json"},
+                                      f"halving, MI355X_MICROARCH.md), {traffic_src}"},
         "cpu_baseline": cpu,
         "parity_sample_bit_exact": parity,
         "variants": variants,
@@ -323,13 +325,14 @@ def bench_allreduce(args):
 
     S = args.mib << 20
     # the communicator's large-Allreduce tuner (mpigx.cpp ar_tune_*) decides
-    # pull vs push two-shot on its first zero-copy calls (registration, pull,
-    # push: time_ar's untimed prelude)
-    _ = time_ar(S, 1, 0)
-    ch, pl, ps = ctypes.c_int(-1), ctypes.c_double(0), ctypes.c_double(0)
-    MPI.lib().mpigx_comm_ar_choice(comm.val, ctypes.byref(ch), ctypes.byref(pl), ctypes.byref(ps))
-    ar_tune = {"choice": {-1: "undecided", 0: "pull two-shot", 1: "push two-shot"}[ch.value],
-               "pull_ns_per_MiB": round(pl.value, 1), "push_ns_per_MiB": round(ps.value, 1),
+    # between the pull, push and pull-push two-shots on its first zero-copy
+    # calls (registration, then one call each: time_ar's untimed prelude)
+    _ = time_ar(S, 2, 0)
+    ch, costs = ctypes.c_int(-1), (ctypes.c_double * 3)()
+    MPI.lib().mpigx_comm_ar_costs(comm.val, ctypes.byref(ch), costs)
+    ar_tune = {"choice": {-1: "undecided", 0: "pull two-shot", 1: "push two-shot", 2: "pull-push two-shot"}[ch.value],
+               "pull_ns_per_MiB": round(costs[0], 1), "push_ns_per_MiB": round(costs[1], 1),
+               "pullpush_ns_per_MiB": round(costs[2], 1),
                "basis": "device time of one 256 MiB call each, max over ranks decides (rank 0's shown)"}
     t, kern, send, recv = time_ar(S, args.steps, args.warmup, keep=True)
     correct = check_sample(recv, S // 4, "timed buffers, default algorithm")
@@ -417,7 +420,7 @@ def bench_allreduce(args):
         xs = rank_input(rank, S // 4)
         xr = torch.empty_like(xs)
         names = ("entry_barrier", "reduce_scatter", "mid_barrier", "allgather", "exit_barrier")
-        for algo in ("pull", "pull_generic", "push"):
+        for algo in ("pull", "pull_generic", "push", "pullpush"):
             MPI.set_knob(comm, "ALGO", algo)
             for _ in range(2):
                 MPI.Allreduce_(xs, xr, MPI.SUM, comm)
@@ -468,7 +471,8 @@ def bench_allreduce(args):
                 sweep[f"{nb >> 10}KiB_{algo}_us"] = round(tw * 1e6, 2)
             MPI.set_knob(comm, "ALGO", None)
         rings = len(M.ring_strides(n, 4))
-        for algo, chans in (("pull", 1), ("pull_generic", 1), ("push", 1), ("ring", 1), ("ring", rings)):
+        for algo, chans in (("pull", 1), ("pull_generic", 1), ("push", 1), ("pullpush", 1), ("ring", 1),
+                            ("ring", rings)):
             MPI.set_knob(comm, "ALGO", algo)
             MPI.set_knob(comm, "RING_CHANNELS", chans)
             tag = algo if algo != "ring" or chans == 1 else f"ring{chans}"

@@ -174,6 +174,8 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
 #define MPIGX_ALGO_PULL 7     /* "pull": the zero-copy pull two-shot (no pull/push tuning) */
 #define MPIGX_ALGO_PULL_GENERIC 8 /* "pull_generic": the same through the all-modes fold kernel
                                      (fewer vectors per thread in flight; comparison only) */
+#define MPIGX_ALGO_PULLPUSH 9 /* "pullpush": zero-copy pull reduce-scatter that stores each reduced
+                                 slice into every rank's recvbuf (no allgather phase) */
 int mpigx_comm_set_knob(mpigx_comm_t comm, int knob, long long value);
 int mpigx_comm_get_knob(mpigx_comm_t comm, int knob, long long *value);
 
@@ -204,9 +206,13 @@ int mpigx_comm_zc_stats(mpigx_comm_t comm, unsigned long long *optimistic_hits,
 int mpigx_comm_host_stats(mpigx_comm_t comm, double *prelaunch_us);
 /* Large (zero-copy-sized) Allreduce algorithm the communicator measured and
  * chose (MPIGX_AR_TUNE): *choice = -1 undecided, 0 pull two-shot, 1 push
- * two-shot; *pull_ns_per_mib / *push_ns_per_mib = this rank's measured device
- * time per MiB of message (0 = not measured).  Diagnostic. */
+ * two-shot, 2 pull-push two-shot (MPIGX_ALGO_PULLPUSH); *pull_ns_per_mib /
+ * *push_ns_per_mib = this rank's measured device time per MiB of message
+ * (0 = not measured).  Diagnostic. */
 int mpigx_comm_ar_choice(mpigx_comm_t comm, int *choice, double *pull_ns_per_mib, double *push_ns_per_mib);
+/* The same with every candidate's cost: ns_per_mib[0..2] = pull, push,
+ * pull-push (this rank's device ns per MiB; 0 = not measured).  Diagnostic. */
+int mpigx_comm_ar_costs(mpigx_comm_t comm, int *choice, double *ns_per_mib);
 /* Smaller collectives (below the zero-copy size), size class
  * log2_bytes = floor(log2(message bytes)) + 64 * kind (kind 0 Allreduce,
  * 1 Bcast, 2 Allgather, 3 Alltoall; the byte movers' class is the per-rank

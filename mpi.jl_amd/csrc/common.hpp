@@ -36,6 +36,11 @@ constexpr int O_NOOP = 17;
 // and every one of the NMAX leaves present (no runtime guards at all).
 enum Shape : int { SH_PRE = 0, SH_POW2 = 1, SH_FULL = 2 };
 
+// Allgather half of the dedicated zero-copy two-shot (kernels.hpp
+// ar_zc_kernel): pull the peers' reduced chunks, or have each owner store its
+// reduced slice into every rank's recvbuf.
+constexpr int AG_PULL = 0, AG_PUSH = 1;
+
 // The local fold's shape and 16-B vectors per thread — ONE rule for the host
 // (grid size) and the launcher (instantiation).  SH_FULL only at NMAX 8 (the
 // 8-buffer headline; n = 16 takes SH_POW2).  U = 4 measured best or tied on

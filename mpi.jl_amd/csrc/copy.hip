@@ -72,7 +72,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
         if (j < m) acc ^= ld16(pv.stage[(r + 1 + j) % n] + lo + 16 * i);
     }
     if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u) reinterpret_cast<u32x4*>(mine)[threadIdx.x] = acc;
-    rank_barrier(pv, ep++);
+    rank_barrier_exit(pv, ep++);
     return 0;
   }
   if (A.mode == C_BCAST_LL || A.mode == C_ALLGATHER_LL || A.mode == C_ALLTOALL_LL) {
@@ -120,7 +120,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     if (r == A.root) block_copy(mine + lo, send + lo, len);
     if (!rank_barrier(pv, ep++)) return 0;
     if (r != A.root) block_copy_u<2 * U>(recv + lo, pv.stage[A.root] + lo, len);
-    rank_barrier(pv, ep++);
+    rank_barrier_exit(pv, ep++);
     return 0;
   }
   char* dsts[NMAX];
@@ -162,7 +162,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
       }
       block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     }
-    rank_barrier(pv, ep++);
+    rank_barrier_exit(pv, ep++);
     return 0;
   }
   if (A.mode == C_ALLGATHER) {
@@ -184,7 +184,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
       }
     }
     block_gather_u<NMAX, U>(dsts, srcs, lens, m);
-    rank_barrier(pv, ep++);
+    rank_barrier_exit(pv, ep++);
     return 0;
   }
   if (A.mode == C_ALLGATHER_ZC) {
@@ -210,7 +210,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
       }
       block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     }
-    rank_barrier(pv, ep++, &ab);
+    rank_barrier_exit(pv, ep++, &ab);
     return ab;
   }
   if (A.mode == C_BCAST_ZC) {
@@ -218,7 +218,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     int ab;
     if (!zc_enter(pv, ep++, &ab)) return 0;
     if (!ab && r != A.root) block_copy_u<2 * U>(recv + lo, A.zsrc[A.root] + lo, len);
-    rank_barrier(pv, ep++, &ab);
+    rank_barrier_exit(pv, ep++, &ab);
     return ab;
   }
   if (A.mode == C_BCAST_SAG_ZC) {
@@ -252,7 +252,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
       }
       block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     }
-    rank_barrier(pv, ep++, &ab);
+    rank_barrier_exit(pv, ep++, &ab);
     return ab;
   }
   if (A.mode == C_ALLTOALL_ZC) {
@@ -276,7 +276,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     }
     block_gather_u<NMAX, U>(dsts, srcs, lens, m);
     }
-    rank_barrier(pv, ep++, &ab);  // nobody reads my sendbuf any more
+    rank_barrier_exit(pv, ep++, &ab);  // nobody reads my sendbuf any more
     return ab;
   }
   // C_ALLTOALL: block p of my send goes to rank p; block j of my recv comes
@@ -298,7 +298,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     }
   }
   block_gather_u<NMAX, U>(dsts, srcs, lens, m);
-  rank_barrier(pv, ep++);
+  rank_barrier_exit(pv, ep++);
   return 0;
 }
 
@@ -348,7 +348,7 @@ __device__ __forceinline__ void vx_body(const VArgs& A) {
     }
   }
   block_gather_u<NMAX, U>(dsts, srcs, lens, m);
-  rank_barrier(pv, ep++);
+  rank_barrier_exit(pv, ep++);
 }
 
 template <int NMAX, int U>

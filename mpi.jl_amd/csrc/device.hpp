@@ -745,6 +745,68 @@ __device__ __forceinline__ void fold_span(const FoldArgs& A, const T* const* src
   for (long long e = lo + nv * W + tid; e < hi; e += nt) fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, e, 1, out, out2);
 }
 
+// fold_span with every folded vector stored into m outputs (outs[0..m-1]:
+// my recvbuf, then the peers' — the push-allgather two-shot, kernels.hpp
+// ar_zc_kernel AG_PUSH).  SH_FULL: m == NMAX, the stores carry no guard.
+// Each element is read (all its leaves) and then written by ONE thread, so
+// in-place buffers (sendbuf == recvbuf on some rank) are safe: no other
+// thread of any rank touches that element.  `vec` false (a pointer not 16-B
+// aligned): scalar folds throughout.
+template <class OP, class T, int NMAX, int SCHED, int SHAPE, int U>
+__device__ __forceinline__ void fold_span_scatter(const FoldArgs& A, const T* const* src, const T* const* src2,
+                                                  long long lo, long long hi, T* const (&outs)[NMAX], int m,
+                                                  bool vec) {
+  constexpr int W = VecW<T>::v;
+  const long long tid = threadIdx.x, nt = blockDim.x;
+  auto put1 = [&](long long e) {  // scalar fold of element e into every output
+    Vec<T, 1> r;
+    fold_at<OP, T, NMAX, SCHED, SHAPE, 1>(A, src, src2, e, r);
+#pragma unroll
+    for (int p = 0; p < NMAX; ++p)
+      if (SHAPE == SH_FULL || p < m) outs[p][e] = r.x[0];
+  };
+  if (!vec) {
+    for (long long e = lo + tid; e < hi; e += nt) put1(e);
+    return;
+  }
+  const long long nv = (hi - lo) / W;
+  long long v0 = tid;
+  for (; v0 + (long long)(U - 1) * nt < nv; v0 += U * nt) {
+    Leaves<T, NMAX, SHAPE, W> L[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_leaves<T, NMAX, SCHED, SHAPE, W>(A, src, src2, lo + (v0 + u * nt) * W, L[u]);
+    unsigned strad = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long e = lo + (v0 + u * nt) * W;
+      Vec<T, W> r;
+      if (fold_leaves<OP, T, NMAX, SCHED, SHAPE, W>(A, e, L[u], r)) {
+#pragma unroll
+        for (int p = 0; p < NMAX; ++p)
+          if (SHAPE == SH_FULL || p < m) stv<T, W>(outs[p] + e, r);
+      } else {
+        strad |= 1u << u;
+      }
+    }
+#pragma unroll 1
+    for (int u = 0; u < U; ++u)
+      if ((strad >> u) & 1u)
+        for (int w = 0; w < W; ++w) put1(lo + (v0 + u * nt) * W + w);
+  }
+  for (; v0 < nv; v0 += nt) {
+    const long long e = lo + v0 * W;
+    Vec<T, W> r;
+    if (fold_at<OP, T, NMAX, SCHED, SHAPE, W>(A, src, src2, e, r)) {
+#pragma unroll
+      for (int p = 0; p < NMAX; ++p)
+        if (SHAPE == SH_FULL || p < m) stv<T, W>(outs[p] + e, r);
+    } else {
+      for (int w = 0; w < W; ++w) put1(e + w);
+    }
+  }
+  for (long long e = lo + nv * W + tid; e < hi; e += nt) put1(e);
+}
+
 // ---------------------------------------------------------------------------
 // Pull kernels launched after a HOST-side hand-off (p2p / RMA: the producer's
 // kernel finished and the host saw it) read peer memory mapped through IPC.
@@ -801,14 +863,14 @@ __device__ __forceinline__ void stamp(const PeerView& pv, int k) {
 }
 
 __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, int* abort = nullptr,
-                                             unsigned key = 0, bool check_key = false) {
+                                             unsigned key = 0, bool check_key = false, bool fences = true) {
   __shared__ int s_fail, s_abort;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int ab_in = abort ? *abort : 0;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bool ok = true, ab = false;
     if (lane < pv.n) {
@@ -829,7 +891,7 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
     }
     const bool all_ok = __all(ok);
     const bool any_ab = __any(ab);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (fences) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (lane == 0) {
       s_fail = all_ok ? 0 : 1;
       s_abort = (ab_in || any_ab) ? 1 : 0;
@@ -839,6 +901,17 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
   __syncthreads();
   if (abort) *abort = s_abort;
   return s_fail == 0;
+}
+
+// The LAST barrier of a pull-only launch means only "no peer reads my memory
+// any more": nothing is published across it (every byte this rank wrote is
+// its own, read by no peer after this point, and the next launch's entry
+// barrier releases again), so it needs no system-scope release (L2
+// write-back) or acquire (L2 invalidate) — only every wave's loads retired
+// (s_waitcnt vmcnt(0) + block barrier) before the flag store.  Not for a
+// launch whose peers STORE into this rank's memory (push two-shot).
+__device__ __forceinline__ bool rank_barrier_exit(const PeerView& pv, uint64_t ep, int* abort = nullptr) {
+  return rank_barrier(pv, ep, abort, 0, false, false);
 }
 
 // Zero-copy launches (mpigx.cpp zc_run): entry barrier with the view key and

@@ -99,25 +99,30 @@ hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs
 // takes (zc_u, kernels.hpp: 8- and 16-bit elements hold one element per
 // VGPR); SH_FULL when every one of the NMAX leaves is present with no
 // pre-step, else SH_PRE.  nmax/shape come from arzc_shape (launch.hpp).
-template <class OP>
-hipError_t arzc_op(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a) {
+template <class OP, int AG>
+hipError_t arzc_ag(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a) {
   if (nmax == 2)
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 2, SH_FULL, zc_u<T>(8)>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 2, SH_FULL, zc_u<T>(8), AG>), grid, dim3(kThreads), 0, s, a);
   else if (nmax == 4 && shape == SH_FULL)
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_FULL, zc_u<T>(4)>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_FULL, zc_u<T>(4), AG>), grid, dim3(kThreads), 0, s, a);
   else if (nmax == 4)
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_PRE, zc_u<T>(4)>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 4, SH_PRE, zc_u<T>(4), AG>), grid, dim3(kThreads), 0, s, a);
   else if (shape == SH_FULL)
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_FULL, zc_u<T>(2)>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_FULL, zc_u<T>(2), AG>), grid, dim3(kThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_PRE, zc_u<T>(2)>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((ar_zc_kernel<OP, T, 8, SH_PRE, zc_u<T>(2), AG>), grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();
+}
+// ag: AG_PULL (pull two-shot) or AG_PUSH (pull reduce-scatter + push allgather)
+template <class OP>
+hipError_t arzc_op(int nmax, int shape, int ag, dim3 grid, hipStream_t s, const FoldArgs& a) {
+  return ag == AG_PUSH ? arzc_ag<OP, AG_PUSH>(nmax, shape, grid, s, a) : arzc_ag<OP, AG_PULL>(nmax, shape, grid, s, a);
 }
 
 // Resident 256-thread blocks per CU of ONE kernel that spins on its peers
 // (the host caps that launch's grid with it, mpigx.cpp kernel_cap).
 //   kind 0 fold_kernel (a = nmax, b = sched), 1 ar_zc_kernel (a = nmax,
-//   b = shape), 2 ring_kernel, 3 scan_kernel
+//   b = shape), 2 ring_kernel, 3 scan_kernel, 4 ar_zc_kernel AG_PUSH
 template <class K>
 int occ1(K k) {
   int nb = 0;
@@ -127,18 +132,22 @@ int occ1(K k) {
   }
   return nb;
 }
+template <class OP, int AG>
+int occ_arzc(int a, int b) {
+  if (a == 2) return occ1(ar_zc_kernel<OP, T, 2, SH_FULL, zc_u<T>(8), AG>);
+  if (a == 4) return b == SH_FULL ? occ1(ar_zc_kernel<OP, T, 4, SH_FULL, zc_u<T>(4), AG>)
+                                  : occ1(ar_zc_kernel<OP, T, 4, SH_PRE, zc_u<T>(4), AG>);
+  return b == SH_FULL ? occ1(ar_zc_kernel<OP, T, 8, SH_FULL, zc_u<T>(2), AG>)
+                      : occ1(ar_zc_kernel<OP, T, 8, SH_PRE, zc_u<T>(2), AG>);
+}
 template <class OP>
 int occ_op(int kind, int a, int b) {
   switch (kind) {
     case 0:
       if (a <= 8) return b == S_LINEAR ? occ1(fold_kernel<OP, T, 8, S_LINEAR>) : occ1(fold_kernel<OP, T, 8, S_TREE>);
       return b == S_LINEAR ? occ1(fold_kernel<OP, T, 16, S_LINEAR>) : occ1(fold_kernel<OP, T, 16, S_TREE>);
-    case 1:
-      if (a == 2) return occ1(ar_zc_kernel<OP, T, 2, SH_FULL, zc_u<T>(8)>);
-      if (a == 4) return b == SH_FULL ? occ1(ar_zc_kernel<OP, T, 4, SH_FULL, zc_u<T>(4)>)
-                                      : occ1(ar_zc_kernel<OP, T, 4, SH_PRE, zc_u<T>(4)>);
-      return b == SH_FULL ? occ1(ar_zc_kernel<OP, T, 8, SH_FULL, zc_u<T>(2)>)
-                          : occ1(ar_zc_kernel<OP, T, 8, SH_PRE, zc_u<T>(2)>);
+    case 1: return occ_arzc<OP, AG_PULL>(a, b);
+    case 4: return occ_arzc<OP, AG_PUSH>(a, b);
     case 2: return occ1(ring_kernel<OP, T>);
     default: return occ1(scan_kernel<OP, T>);
   }
@@ -150,7 +159,7 @@ int occ_op(int kind, int a, int b) {
 #define MPIGX_ARZC_FN(K) MPIGX_CAT4(launch_arzc_, MPIGX_REP_NAME, _o, K)
 #define MPIGX_OCC_FN(K) MPIGX_CAT4(occupancy_, MPIGX_REP_NAME, _o, K)
 #define MPIGX_DECL_OP(K)                                                                               \
-  hipError_t MPIGX_ARZC_FN(K)(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a);      \
+  hipError_t MPIGX_ARZC_FN(K)(int nmax, int shape, int ag, dim3 grid, hipStream_t s, const FoldArgs& a);      \
   int MPIGX_OCC_FN(K)(int kind, int a, int b);                                                         \
   hipError_t MPIGX_FOLD_FN(K)(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a);      \
   hipError_t MPIGX_RING_FN(K)(dim3 grid, hipStream_t s, const RingArgs& a);                            \
@@ -166,8 +175,8 @@ MPIGX_DECL_OP(6) MPIGX_DECL_OP(7) MPIGX_DECL_OP(8) MPIGX_DECL_OP(9) MPIGX_DECL_O
     if constexpr (valid_op(K)) return fold_op<OpOf<K>::type>(nmax, sched, grid, s, a);                 \
     return hipErrorInvalidValue;                                                                       \
   }                                                                                                    \
-  hipError_t MPIGX_ARZC_FN(K)(int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a) {     \
-    if constexpr (valid_op(K)) return arzc_op<OpOf<K>::type>(nmax, shape, grid, s, a);                 \
+  hipError_t MPIGX_ARZC_FN(K)(int nmax, int shape, int ag, dim3 grid, hipStream_t s, const FoldArgs& a) { \
+    if constexpr (valid_op(K)) return arzc_op<OpOf<K>::type>(nmax, shape, ag, grid, s, a);             \
     return hipErrorInvalidValue;                                                                       \
   }                                                                                                    \
   int MPIGX_OCC_FN(K)(int kind, int a, int b) {                                                        \
@@ -252,9 +261,9 @@ hipError_t MPIGX_CAT(launch_fold_, MPIGX_REP_NAME)(int op, int nmax, int sched, 
                                                   const FoldArgs& a) {
   MPIGX_SWITCH(MPIGX_FOLD_FN, nmax, sched, grid, s, a)
 }
-hipError_t MPIGX_CAT(launch_arzc_, MPIGX_REP_NAME)(int op, int nmax, int shape, dim3 grid, hipStream_t s,
+hipError_t MPIGX_CAT(launch_arzc_, MPIGX_REP_NAME)(int op, int nmax, int shape, int ag, dim3 grid, hipStream_t s,
                                                   const FoldArgs& a) {
-  MPIGX_SWITCH(MPIGX_ARZC_FN, nmax, shape, grid, s, a)
+  MPIGX_SWITCH(MPIGX_ARZC_FN, nmax, shape, ag, grid, s, a)
 }
 int MPIGX_CAT(occupancy_, MPIGX_REP_NAME)(int op, int kind, int a, int b) {
   switch (op) {

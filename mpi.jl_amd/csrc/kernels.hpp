@@ -210,7 +210,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
     }
     stamp(pv, 4);
-    rank_barrier(pv, ep++, &ab);  // nobody reads my buffers any more
+    rank_barrier_exit(pv, ep++, &ab);  // nobody reads my buffers any more
     stamp(pv, 5);
     return ab;
   }
@@ -261,7 +261,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       }
       block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
     }
-    rank_barrier(pv, ep++, &ab);  // nobody reads my sendbuf / arena any more
+    rank_barrier_exit(pv, ep++, &ab);  // nobody reads my sendbuf / arena any more
     return ab;
   }
 
@@ -429,7 +429,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     if (!rank_barrier(pv, ep++)) return 0;
     if (A.mode == M_AR_ONESHOT || pv.rank == A.root)
       fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
-    rank_barrier(pv, ep++);
+    rank_barrier_exit(pv, ep++);
     return 0;
   }
 
@@ -477,7 +477,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     }
     block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
   }
-  rank_barrier(pv, ep++);
+  rank_barrier_exit(pv, ep++);
   return 0;
 }
 
@@ -499,8 +499,14 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
 // M_AR_ZC (identical bits; that path still serves LINEAR order and n > 8).
 // SHAPE: SH_FULL (n = NMAX, no pre-step: every leaf present, no guards) or
 // SH_PRE (pre-step partners and / or fewer leaves, guarded).
+// AG: AG_PULL as above; AG_PUSH ("pullpush", MPIGX_ALGO=pullpush) stores each
+// reduced slice straight into EVERY rank's recvbuf during the fold (peers'
+// through the view's mappings) — no mid barrier, no allgather reads: per rank
+// read S + write S instead of read 1.5 S + write S at n = 2 (2 S + 7/8 S
+// reads at n = 8), the same xGMI bytes with the allgather half as posted
+// writes.  Its exit barrier publishes those stores (full release / acquire).
 // ---------------------------------------------------------------------------
-template <class OP, class T, int NMAX, int SHAPE, int U>
+template <class OP, class T, int NMAX, int SHAPE, int U, int AG = AG_PULL>
 __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
   __shared__ FoldArgs A;  // indexed by runtime ranks below (see fold_kernel)
   {
@@ -535,10 +541,31 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
       for (int s = 0; s < NMAX / 2; ++s)
         if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
     }
-    if (vec) fold_span<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, hi, recv, nullptr);
-    else fold_range<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, lo, hi, recv, nullptr, false, tid, nt);
+    if constexpr (AG == AG_PUSH) {
+      T* outs[NMAX];  // mine first, then the peers' recvbufs
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j) {
+        outs[j] = recv;
+        if (j > 0 && j < n) {
+          outs[j] = (T*)A.zc_recv[(r + j) % n];
+          vec &= ((uintptr_t)outs[j] & 15) == 0;
+        }
+      }
+      fold_span_scatter<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, hi, outs, n, vec);
+    } else {
+      if (vec) fold_span<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, hi, recv, nullptr);
+      else fold_range<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, lo, hi, recv, nullptr, false, tid, nt);
+    }
   }
   stamp(pv, 2);
+  if constexpr (AG == AG_PUSH) {
+    stamp(pv, 3);
+    stamp(pv, 4);
+    rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
+    stamp(pv, 5);
+    signal_done(pv, ab);
+    return;
+  }
   if (!rank_barrier(pv, ep++, &ab)) {  // every reduced chunk is in its owner's recvbuf
     signal_done(pv, 0);
     return;
@@ -566,7 +593,7 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
     block_gather_u<MP, U>(dsts, srcs, lens, n - 1);
   }
   stamp(pv, 4);
-  rank_barrier(pv, ep++, &ab);  // nobody reads my buffers any more
+  rank_barrier_exit(pv, ep++, &ab);  // nobody reads my buffers any more
   stamp(pv, 5);
   signal_done(pv, ab);
 }
@@ -685,7 +712,7 @@ __device__ __forceinline__ int ring_body(const RingArgs& A) {  // returns the ab
   } else {
     ep += 2 * n - 3;  // every rank aborted at the entry: same epochs, no ring traffic
   }
-  rank_barrier(pv, ep++, &ab);  // nobody reads my buffers / arena any more
+  rank_barrier_exit(pv, ep++, &ab);  // nobody reads my buffers / arena any more
   return ab;
 }
 
@@ -823,7 +850,7 @@ __device__ __forceinline__ int scan_body(const ScanArgs& A) {  // returns the ab
     }
   }
   if (A.ll) return 0;
-  rank_barrier(pv, ep++, &ab);
+  rank_barrier_exit(pv, ep++, &ab);
   return ab;
 }
 

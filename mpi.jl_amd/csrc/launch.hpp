@@ -13,9 +13,10 @@ using AccLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const AccAr
 using ScanLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const ScanArgs& a);
 using RingLauncher = hipError_t (*)(int op, dim3 grid, hipStream_t s, const RingArgs& a);
 
-using ArzcLauncher = hipError_t (*)(int op, int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a);
+// ag: AG_PULL 0 / AG_PUSH 1 (kernels.hpp ar_zc_kernel)
+using ArzcLauncher = hipError_t (*)(int op, int nmax, int shape, int ag, dim3 grid, hipStream_t s, const FoldArgs& a);
 // resident blocks per CU of one spinning kernel: (op, kind 0 fold / 1 ar_zc /
-// 2 ring / 3 scan, a, b) — kern_rep.hip occ_op
+// 2 ring / 3 scan / 4 ar_zc AG_PUSH, a, b) — kern_rep.hip occ_op
 using OccQuery = int (*)(int op, int kind, int a, int b);
 
 // ar_zc_kernel (kernels.hpp) instantiation for a communicator of n <= 8
@@ -30,7 +31,7 @@ inline bool arzc_shape(int n, int ntree, int rem, int* nmax, int* shape) {
 }
 
 #define MPIGX_DECL_REP(NAME)                                                                     \
-  hipError_t launch_arzc_##NAME(int op, int nmax, int shape, dim3 grid, hipStream_t s, const FoldArgs& a); \
+  hipError_t launch_arzc_##NAME(int op, int nmax, int shape, int ag, dim3 grid, hipStream_t s, const FoldArgs& a); \
   int occupancy_##NAME(int op, int kind, int a, int b); \
   hipError_t launch_fold_##NAME(int op, int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a); \
   hipError_t launch_scan_##NAME(int op, dim3 grid, hipStream_t s, const ScanArgs& a); \

@@ -163,9 +163,10 @@ ArzcLauncher arzc_launcher(Rep r) {
 // Resident 256-thread blocks per CU of ONE kernel that spins on its peers
 // (hipOccupancyMaxActiveBlocksPerMultiprocessor; process-wide cache): kind
 // 0 fold_kernel (a = nmax, b = sched), 1 ar_zc_kernel (a = nmax, b = shape),
-// 2 ring_kernel, 3 scan_kernel (kern_rep.hip occ_op), 10 copy_kernel and
+// 2 ring_kernel, 3 scan_kernel, 4 ar_zc_kernel AG_PUSH (kern_rep.hip
+// occ_op), 10 copy_kernel and
 // 11 vx_kernel of an a-rank communicator (copy.hip).
-enum OccKind { OK_FOLD = 0, OK_ARZC = 1, OK_RING = 2, OK_SCAN = 3, OK_COPY = 10, OK_VX = 11 };
+enum OccKind { OK_FOLD = 0, OK_ARZC = 1, OK_RING = 2, OK_SCAN = 3, OK_ARZC_PUSH = 4, OK_COPY = 10, OK_VX = 11 };
 int kernel_occ(int rep, int op, int kind, int a, int b) {
   static std::mutex mu;
   static std::vector<std::pair<unsigned long long, int>> cache;
@@ -346,8 +347,8 @@ int kernel_cap(mpigx_comm* c, int occ) {
 int cap_fold(mpigx_comm* c, const TypeInfo* t, int oc, int nmax, int sched) {
   return kernel_cap(c, kernel_occ(t->rep, oc, OK_FOLD, nmax, sched));
 }
-int cap_arzc(mpigx_comm* c, const TypeInfo* t, int oc, int nmax, int shape) {
-  return kernel_cap(c, kernel_occ(t->rep, oc, OK_ARZC, nmax, shape));
+int cap_arzc(mpigx_comm* c, const TypeInfo* t, int oc, int nmax, int shape, int ag) {
+  return kernel_cap(c, kernel_occ(t->rep, oc, ag == AG_PUSH ? OK_ARZC_PUSH : OK_ARZC, nmax, shape));
 }
 int cap_ring(mpigx_comm* c, const TypeInfo* t, int oc) { return kernel_cap(c, kernel_occ(t->rep, oc, OK_RING, 0, 0)); }
 int cap_scan(mpigx_comm* c, const TypeInfo* t, int oc) { return kernel_cap(c, kernel_occ(t->rep, oc, OK_SCAN, 0, 0)); }
@@ -690,7 +691,11 @@ void zc_apply(PeerView& pv, const ZcLaunch& z) {
 
 // Zero-copy two-shot Allreduce over the whole message (no rounds: nothing is
 // staged).  Same chunk/slice partition and fold schedule as M_AR_TWOSHOT.
-int allreduce_zc(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeInfo* t, int oc) {
+// push_ag: the pull-push variant (ar_zc_kernel AG_PUSH: the reduce-scatter
+// stores into every rank's recvbuf); it needs the dedicated kernel and every
+// buffer 16-B aligned (the same test on every rank: the view's pointers are
+// the agreed ones), otherwise the pull two-shot runs.
+int allreduce_zc(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeInfo* t, int oc, bool push_ag) {
   const int n = c->n, es = t->size;
   const int vec = es >= 16 ? 1 : 16 / es;
   FoldArgs a;
@@ -714,15 +719,18 @@ int allreduce_zc(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeIn
   int znmax, zshape;
   const bool dedicated =
       sched == S_TREE && c->algo != MPIGX_ALGO_PULL_GENERIC && arzc_shape(n, a.ntree, a.rem, &znmax, &zshape);
-  const int grid = grid_for(c, a.chunk * es, dedicated ? cap_arzc(c, t, oc, znmax, zshape)
+  bool aligned = true;
+  for (int p = 0; p < n; ++p) aligned &= (((uintptr_t)z.ps[p] | (uintptr_t)z.pr[p]) & 15) == 0;
+  const int ag = (push_ag && dedicated && aligned) ? AG_PUSH : AG_PULL;
+  const int grid = grid_for(c, a.chunk * es, dedicated ? cap_arzc(c, t, oc, znmax, zshape, ag)
                                                         : cap_fold(c, t, oc, nmax, sched));
   a.slice = rup(cdiv(a.chunk, grid), vec);
   if (dedicated)
-    HIPCK(arzc_launcher(t->rep)(oc, znmax, zshape, dim3(grid), c->stream, a));
+    HIPCK(arzc_launcher(t->rep)(oc, znmax, zshape, ag, dim3(grid), c->stream, a));
   else
     HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
   note_launch(c, a.pv, grid);
-  c->epoch += 3;
+  c->epoch += ag == AG_PUSH ? 2 : 3;
   return MPIGX_SUCCESS;
 }
 
@@ -914,26 +922,29 @@ void ll_launched(mpigx_comm* c) {
 bool copy_ll_take(mpigx_comm* c, long long bytes) { return ll_fits(c, bytes); }
 
 // Large-Allreduce tuner.  Whether pulling peer data over xGMI (two-shot,
-// M_AR_ZC) or pushing it (M_AR_PUSH) moves more bytes per second depends on
-// the fabric, so the communicator measures both on its first zero-copy-sized
-// Allreduces (blocking calls only: the host then knows the launch finished)
-// and keeps the faster.  Device time of the launch, max over ranks (one host
-// exchange), per byte; push must win by 3 % to replace the pull.  Both give
-// the same bits (same fold schedule), so the choice never changes results.
-// Returns the variant to time on this call (0 pull, 1 push) or -1.  Every
-// rank sees the same calls and outcomes (blocking mode, MPIGX_AR_TUNE and the
-// zero-copy verdict agree), so the exchange in ar_tune_note is collective.
-int ar_tune_pick(mpigx_comm* c, bool* push) {
+// M_AR_ZC), pushing it (M_AR_PUSH) or pulling the reduce-scatter and pushing
+// the allgather (ar_zc_kernel AG_PUSH) moves more bytes per second depends on
+// the fabric, so the communicator measures the three on its first
+// zero-copy-sized Allreduces (blocking calls only: the host then knows the
+// launch finished) and keeps the fastest.  Device time of the launch, max
+// over ranks (one host exchange), per byte; another variant must beat the
+// pull by 3 % to replace it.  All give the same bits (same fold schedule),
+// so the choice never changes results.  Returns the variant to time on this
+// call (0 pull, 1 push, 2 pull-push) or -1 and sets *variant to the one to
+// run.  Every rank sees the same calls and outcomes (blocking mode,
+// MPIGX_AR_TUNE and the zero-copy verdict agree), so the exchange in
+// ar_tune_note is collective.
+int ar_tune_pick(mpigx_comm* c, int* variant) {
   if (c->ar_choice >= 0) {
-    *push = c->ar_choice == 1;
+    *variant = c->ar_choice;
     return -1;
   }
-  *push = false;
+  *variant = 0;
   if (!c->ar_tune || !c->blocking || c->sync_mode != 1 || !c->ar_ev[0]) return -1;
   const int step = c->ar_step++;
   if (step == 0) return -1;  // registration call (host exchange, first imports)
-  *push = step % 2 == 0;     // pull, push, (pull, push ... if a call fell back to staging)
-  return *push ? 1 : 0;
+  *variant = (step - 1) % 3;  // pull, push, pull-push (again if a call fell back to staging)
+  return *variant;
 }
 int ar_tune_note(mpigx_comm* c, int variant, long long bytes) {
   float ms = 0;
@@ -941,14 +952,15 @@ int ar_tune_note(mpigx_comm* c, int variant, long long bytes) {
   HIPCK(hipEventSynchronize(c->ar_ev[1]));
   HIPCK(hipEventElapsedTime(&ms, c->ar_ev[0], c->ar_ev[1]));
   c->ar_spb[variant] = (ms / 1e3) / (double)bytes;
-  if (variant != 1 || c->ar_spb[0] <= 0) return MPIGX_SUCCESS;
-  double mine[2] = {c->ar_spb[0], c->ar_spb[1]}, all[kMaxRanks][2];
+  if (variant != 2 || c->ar_spb[0] <= 0 || c->ar_spb[1] <= 0) return MPIGX_SUCCESS;
+  double mine[3] = {c->ar_spb[0], c->ar_spb[1], c->ar_spb[2]}, all[kMaxRanks][3];
   const int rc = host_allgather(c, mine, sizeof mine, all);
   if (rc) return rc;
-  double w[2] = {0, 0};
+  double w[3] = {0, 0, 0};
   for (int q = 0; q < c->n; ++q)
-    for (int k = 0; k < 2; ++k) w[k] = all[q][k] > w[k] ? all[q][k] : w[k];
-  c->ar_choice = w[1] < 0.97 * w[0] ? 1 : 0;
+    for (int k = 0; k < 3; ++k) w[k] = all[q][k] > w[k] ? all[q][k] : w[k];
+  int best = w[1] < w[2] ? 1 : 2;
+  c->ar_choice = w[best] < 0.97 * w[0] ? best : 0;
   return MPIGX_SUCCESS;
 }
 
@@ -1059,17 +1071,18 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
   const int algo = c->algo;  // knob: identical on every rank
   // count and the thresholds are identical on every rank, so is this test
   if (all && n > 1 && c->zc_min > 0 && count * es >= c->zc_min && algo != MPIGX_ALGO_ONESHOT) {
-    bool push = algo == MPIGX_ALGO_PUSH;
+    int variant = algo == MPIGX_ALGO_PUSH ? 1 : algo == MPIGX_ALGO_PULLPUSH ? 2 : 0;
     const bool ring = algo == MPIGX_ALGO_RING;
-    // no MPIGX_ALGO: the pull or the push two-shot, whichever measured faster
-    // on this communicator (ar_tune_*); undecided, call 2 times the pull and
-    // call 3 the push (call 1 registers the buffers)
-    const int timed = algo != MPIGX_ALGO_AUTO ? -1 : ar_tune_pick(c, &push);
+    // no MPIGX_ALGO: the pull, push or pull-push two-shot, whichever measured
+    // fastest on this communicator (ar_tune_*); undecided, calls 2-4 time
+    // them in turn (call 1 registers the buffers)
+    const int timed = algo != MPIGX_ALGO_AUTO ? -1 : ar_tune_pick(c, &variant);
     bool staged;
     const int rc = zc_run(c, send, recv, &staged, [&](const ZcLaunch& z) {
       if (ring) return allreduce_ring(c, z, count, t, oc);
       if (timed >= 0) HIPCK(hipEventRecord(c->ar_ev[0], c->stream));
-      const int lr = push ? allreduce_push(c, z, send, count, t, oc) : allreduce_zc(c, z, count, t, oc);
+      const int lr = variant == 1 ? allreduce_push(c, z, send, count, t, oc)
+                                  : allreduce_zc(c, z, count, t, oc, variant == 2);
       if (timed >= 0 && !lr) HIPCK(hipEventRecord(c->ar_ev[1], c->stream));
       return lr;
     });
@@ -1484,7 +1497,8 @@ namespace {
 // Every path-selecting setting is read ONCE, here, per communicator; init
 // compares every rank's values (comm_init) and mpigx_comm_set_knob changes
 // them only collectively, so all ranks always take the same branch.
-const char* const kAlgoNames[] = {"", "ll", "ll2", "oneshot", "twoshot", "push", "ring", "pull", "pull_generic"};
+const char* const kAlgoNames[] = {"",     "ll",   "ll2",  "oneshot",      "twoshot",
+                                  "push", "ring", "pull", "pull_generic", "pullpush"};
 const char* const kKnobEnv[MPIGX_KNOB_COUNT] = {
     "MPIGX_ALGO",   "MPIGX_BCAST",      "MPIGX_RING_CHANNELS", "MPIGX_MAX_BLOCKS",     "MPIGX_ONESHOT_MAX",
     "MPIGX_ZC_MIN", "MPIGX_BCAST_SAG_MIN", "MPIGX_ZC_REQUIRE", "MPIGX_BYTES_PER_BLOCK", "MPIGX_LL_AUTO",
@@ -1517,7 +1531,7 @@ int knob_apply(mpigx_comm* c, int k, long long v, bool init) {
   auto in = [&](long long lo, long long hi) { return v >= lo && v <= hi; };
   switch (k) {
     case MPIGX_KNOB_ALGO:
-      if (!in(MPIGX_ALGO_AUTO, MPIGX_ALGO_PULL_GENERIC)) return MPIGX_ERR_ARG;
+      if (!in(MPIGX_ALGO_AUTO, MPIGX_ALGO_PULLPUSH)) return MPIGX_ERR_ARG;
       c->algo = (int)v;
       return MPIGX_SUCCESS;
     case MPIGX_KNOB_BCAST:
@@ -2005,6 +2019,13 @@ int mpigx_comm_ar_choice(mpigx_comm_t c, int* choice, double* pull_ns_per_mib, d
   if (choice) *choice = c->ar_choice;
   if (pull_ns_per_mib) *pull_ns_per_mib = c->ar_spb[0] * 1e9 * 1048576.0;
   if (push_ns_per_mib) *push_ns_per_mib = c->ar_spb[1] * 1e9 * 1048576.0;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_ar_costs(mpigx_comm_t c, int* choice, double* ns_per_mib) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (choice) *choice = c->ar_choice;
+  if (ns_per_mib)
+    for (int k = 0; k < 3; ++k) ns_per_mib[k] = c->ar_spb[k] * 1e9 * 1048576.0;
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_tune_class(mpigx_comm_t c, int log2_bytes, int* choice, double* ns_per_mib) {

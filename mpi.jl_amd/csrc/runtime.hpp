@@ -136,11 +136,11 @@ struct mpigx_comm {
   unsigned long long ll_seq = 0;  // LL launches so far (parity = ll_seq & 1; same on every rank)
   bool ll_unfenced = false;       // an LL launch (no exit barrier) since the last push two-shot
   // large-Allreduce algorithm chosen by measurement (mpigx.cpp ar_tune_*):
-  // -1 undecided, 0 pull two-shot, 1 push two-shot
+  // -1 undecided, 0 pull two-shot, 1 push two-shot, 2 pull-push two-shot
   int ar_choice = -1;
   int ar_tune = 1;                // MPIGX_AR_TUNE
   int ar_step = 0;                // zero-copy Allreduces seen while undecided
-  double ar_spb[2] = {0, 0};      // device seconds per byte: pull, push (this rank)
+  double ar_spb[3] = {0, 0, 0};   // device seconds per byte: pull, push, pull-push (this rank)
   hipEvent_t ar_ev[2] = {nullptr, nullptr};
   // small / medium Allreduce tuner (mpigx.cpp mt_*): per size class
   // (floor(log2 bytes)) the measured choice among LL / one-shot / two-shot

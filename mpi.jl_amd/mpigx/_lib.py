@@ -53,6 +53,7 @@ PROTOTYPES = {
     "mpigx_comm_host_stats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "mpigx_comm_ar_choice": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double)]),
+    "mpigx_comm_ar_costs": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double)]),
     "mpigx_comm_tune_class": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double)]),
     "mpigx_comm_probe": (c_int, [c_void_p, c_int, c_longlong, ctypes.POINTER(ctypes.c_double)]),
     "mpigx_barrier": (c_int, [c_void_p]),

@@ -32,7 +32,7 @@ IN_PLACE = ctypes.c_void_p(-1 & ((1 << 64) - 1))
 # "oneshot"/"twoshot" force the staged algorithms
 # "pull_generic": the zero-copy pull two-shot through the all-modes fold
 # kernel instead of its dedicated kernel (ar_zc_kernel)
-AR_ALGOS = ("ll", "ll2", "oneshot", "twoshot") + (("push", "pull_generic") if os.environ.get("MPIGX_ZC_MIN") else ())
+AR_ALGOS = ("ll", "ll2", "oneshot", "twoshot") + (("push", "pull_generic", "pullpush") if os.environ.get("MPIGX_ZC_MIN") else ())
 
 
 def dev(a):

@@ -31,7 +31,7 @@ from oracle import mpich_model as M  # noqa: E402
 # every MPIGX_ALGO at 16 MiB and 1 MiB; "auto" = the size's own choice
 # (tuners included); where an algorithm cannot take a size the engine runs
 # the static choice (e.g. "ll" above its 256 KiB capacity)
-ALGOS = ("auto", "ll", "ll2", "oneshot", "twoshot", "push", "ring", "pull", "pull_generic")
+ALGOS = ("auto", "ll", "ll2", "oneshot", "twoshot", "push", "ring", "pull", "pull_generic", "pullpush")
 
 
 def extra(comm, r, n, f32_input, fails):
@@ -48,7 +48,7 @@ def extra(comm, r, n, f32_input, fails):
         for algo in ALGOS:
             MPI.set_knob(comm, "ALGO", None if algo == "auto" else algo)
             recv = torch.empty_like(xs[r])
-            for _ in range(3 if algo == "auto" else 1):  # auto: the tuners' sampling calls too
+            for _ in range(4 if algo == "auto" else 1):  # auto: the tuners' sampling calls too
                 recv.zero_()
                 MPI.Allreduce_(xs[r], recv, MPI.SUM, comm)
                 got = recv.cpu().numpy()
@@ -116,17 +116,18 @@ def main():
     if not torch.equal(again.view(torch.int32), recv.view(torch.int32)):
         fails.append(("allreduce-repeat",))
     # the large-Allreduce tuner: call 2 above timed the pull two-shot, call 3
-    # times the push two-shot and decides, call 4 runs the choice; every call
-    # gives the same bits (same fold schedule)
+    # times the push two-shot, call 4 the pull-push two-shot and decides,
+    # call 5 runs the choice; every call gives the same bits (same fold
+    # schedule)
     import ctypes
-    for k in (3, 4):
+    for k in (3, 4, 5):
         again.zero_()
         MPI.Allreduce_(send, again, MPI.SUM, comm)
         if not torch.equal(again.view(torch.int32), recv.view(torch.int32)):
             fails.append(("allreduce-tuner-call", k))
     ch = ctypes.c_int(-2)
     MPI.lib().mpigx_comm_ar_choice(comm.val, ctypes.byref(ch), None, None)
-    if ch.value not in (0, 1):
+    if ch.value not in (0, 1, 2):
         fails.append(("ar-tune-undecided", ch.value))
     del send, recv, again, xs
 

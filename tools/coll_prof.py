@@ -96,7 +96,10 @@ def algo_bytes(algo, n, S):
     pull / ring: per rank RS reads n chunks of S/n and writes S/n, AG reads and
     writes (n-1)S/n -> S(2 + (n-1)/n).  push: per rank phase 1 reads and writes
     (n-1)S/n (peers' arena slots), phase 2 reads S (slots + own chunk) and
-    writes S (own + peers' recvbufs) -> 2S(1 + (n-1)/n)."""
+    writes S (own + peers' recvbufs) -> 2S(1 + (n-1)/n).  pullpush: per rank
+    the fold reads n chunks of S/n and writes its chunk into n recvbufs -> 2S."""
+    if algo == "pullpush":
+        return n * 2 * S
     if algo == "push":
         return n * 2 * S * (1 + (n - 1) / n)
     return n * S * (2 + (n - 1) / n)
@@ -107,8 +110,8 @@ def main():
     ap.add_argument("out")
     ap.add_argument("tag")
     ap.add_argument("--n", type=int, default=2)
-    ap.add_argument("--configs", default="256:pull,256:pull_generic,256:push,256:ring,16:pull,16:pull_generic")
-    ap.add_argument("--pmc-configs", default="256:pull,256:pull_generic,256:push,16:pull")
+    ap.add_argument("--configs", default="256:pull,256:pullpush,256:pull_generic,256:push,256:ring,16:pull,16:pullpush")
+    ap.add_argument("--pmc-configs", default="256:pull,256:pullpush,16:pull")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--timeout", type=int, default=150)
     a = ap.parse_args()
