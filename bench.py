@@ -129,6 +129,33 @@ def traffic_from_profiles(key):
     return best, src
 
 
+def coll_hbm_bytes(kind, n, S):
+    """Algorithmic HBM bytes of one S-byte Allreduce, all n ranks on one GPU
+    (tools/coll_prof.py algo_bytes): pull two-shot S(2 + (n-1)/n) per rank,
+    pull-push 2S, push 2S(1 + (n-1)/n)."""
+    if kind == "pullpush":
+        return 2 * n * S
+    if kind == "push":
+        return 2 * n * S * (1 + (n - 1) / n)
+    return n * S * (2 + (n - 1) / n)
+
+
+def coll_traffic_from_profiles(kind, n, mib):
+    """(HBM bytes of one call, all ranks, file) from the newest committed
+    collective-kernel PMC profile (profiles/*_coll_n<n>_1gpu.json, tools/coll_prof.py)."""
+    import glob
+    best, src = None, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_coll_n{n}_1gpu.json"))):
+        try:
+            t = json.load(open(f))["configs"].get(f"{mib}:{kind}", {}).get("traffic") or {}
+        except Exception:
+            continue
+        for k, v in t.items():
+            if "ar_zc_kernel" in k:
+                best, src = v["hbm_bytes_rank0"] * n, os.path.relpath(f, ROOT)
+    return best, src
+
+
 def bench_local(args):
     import torch
     import mpigx as MPI
@@ -615,16 +642,24 @@ def bench_allreduce(args):
     ach = busbw(S, kern)
     peak_nom = XGMI_LINK_GBPS * (n - 1)
     if same_device:
-        roof = {"bound": "hbm (same-device IPC)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
-                "note": "all ranks share one GPU: peer pulls are HBM reads through IPC mappings, no xGMI"}
+        # every rank's kernel streams the same HBM: achieved = the chosen
+        # variant's algorithmic HBM bytes of one call, all ranks, / device time
+        kind = {"pull-push two-shot": "pullpush", "push two-shot": "push"}.get(ar_tune["choice"], "pull")
+        hbm_b = coll_hbm_bytes(kind, n, S)
+        traffic, traffic_src = coll_traffic_from_profiles(kind, n, args.mib)
+        roof = {"bound": "hbm (same-device IPC)", "achieved": round(hbm_b / kern / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(hbm_b / kern / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": f"ar_zc_kernel ({kind})", "algorithmic_hbm_bytes_per_call": hbm_b,
+                "busbw_device_GBps": round(ach, 1),
+                "traffic_basis": f"rocprofv3 PMC of rank 0's kernel x {n} ranks, {traffic_src}" if traffic_src else None,
+                "note": "all ranks share one GPU: peer pulls / pushes are HBM accesses through IPC mappings, no xGMI"}
     else:
         roof = {"bound": "xgmi", "achieved": round(ach, 1), "peak": round(peak_nom, 1), "unit": "GB/s",
                 "frac": round(ach / peak_nom, 4),
                 "traffic": xg["read_bytes_per_step"] if xg else None,
                 "peak_basis": f"nominal {n - 1} links x {XGMI_LINK_GBPS} GB/s per direction (MI355X spec)"}
-    roof.update({"achieved_basis": "busbw of the blocking call's device time (HIP events around each call on the "
-                                   "comm stream), max over ranks",
+    roof.update({"achieved_basis": ("algorithmic HBM bytes of one call (all ranks) / " if same_device else "busbw of ")
+                 + "the blocking call's device time (HIP events around each call on the comm stream), max over ranks",
                  "xgmi_traffic": xg})
     if rank == 0:
         res = {
