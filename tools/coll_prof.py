@@ -41,7 +41,7 @@ def free_port():
     return p
 
 
-def run_ranks(n, mib, algo, prof, outdir, iters, timeout):
+def run_ranks(n, mib, algo, prof, outdir, iters, timeout, slices=None):
     """prof(rank) -> rocprofv3 argument list (or None).  Returns rank 0's JSON."""
     port = free_port()
     procs = []
@@ -49,7 +49,7 @@ def run_ranks(n, mib, algo, prof, outdir, iters, timeout):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), TMPDIR="/tmp", MPIGX_DEVICE="0", MPIGX_TIMEOUT_MS="20000")
         cmd = [sys.executable, os.path.join(ROOT, "tools", "coll_rank.py"), "--mib", str(mib), "--algo", algo,
-               "--iters", str(iters)]
+               "--iters", str(iters)] + ([] if slices is None else ["--slices", str(slices)])
         p = prof(r)
         if p:
             cmd = ["rocprofv3", *p, "-d", os.path.join(outdir, f"rank{r}"), "-o", "run", "--output-format", "csv",
@@ -98,7 +98,7 @@ def algo_bytes(algo, n, S):
     (n-1)S/n (peers' arena slots), phase 2 reads S (slots + own chunk) and
     writes S (own + peers' recvbufs) -> 2S(1 + (n-1)/n).  pullpush: per rank
     the fold reads n chunks of S/n and writes its chunk into n recvbufs -> 2S."""
-    if algo == "pullpush":
+    if algo.startswith("pullpush"):
         return n * 2 * S
     if algo == "push":
         return n * 2 * S * (1 + (n - 1) / n)
@@ -122,11 +122,16 @@ def main():
     for cfg in a.configs.split(","):
         mib, algo = cfg.split(":")
         mib = int(mib)
+        slices = None
+        if "/" in algo:  # "pullpush/0": with MPIGX_AR_SLICES = 0
+            algo, sl = algo.split("/")
+            slices = int(sl)
+        tag = algo if slices is None else f"{algo}_s{slices}"
         S = mib << 20
         rec = {}
-        d = os.path.join(a.out, f"{mib}MiB_{algo}_trace")
+        d = os.path.join(a.out, f"{mib}MiB_{tag}_trace")
         os.makedirs(d, exist_ok=True)
-        res = run_ranks(a.n, mib, algo, lambda r: ["--kernel-trace", "--stats"], d, a.iters, a.timeout)
+        res = run_ranks(a.n, mib, algo, lambda r: ["--kernel-trace", "--stats"], d, a.iters, a.timeout, slices)
         rec["run"] = res
         rows = kernel_rows(d)
         rec["kernels"] = {k: {"dispatches": len(v), "avg_us": round(statistics.mean(v), 2),
@@ -136,10 +141,10 @@ def main():
         if cfg in pmc_set:
             tr = {}
             for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-                dp = os.path.join(a.out, f"{mib}MiB_{algo}_{counter.lower()}")
+                dp = os.path.join(a.out, f"{mib}MiB_{tag}_{counter.lower()}")
                 os.makedirs(dp, exist_ok=True)
                 run_ranks(a.n, mib, algo, lambda r, c=counter: ["--pmc", c, "--kernel-trace"] if r == 0 else None,
-                          dp, 5, a.timeout)
+                          dp, 5, a.timeout, slices)
                 for k, v in pmc(dp, counter).items():
                     tr.setdefault(k, {})[counter + "_KB_median"] = statistics.median(v)
             for k, v in tr.items():

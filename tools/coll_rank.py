@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--algo", default="pull")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--slices", type=int, default=None, help="MPIGX_AR_SLICES knob (pull-push two-shot)")
     args = ap.parse_args()
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
@@ -43,6 +44,8 @@ def main():
     comm = MPI.Init()
     if args.algo != "auto":
         MPI.set_knob(comm, "ALGO", args.algo)
+    if args.slices is not None:
+        MPI.set_knob(comm, "AR_SLICES", args.slices)
     dev = torch.device("cuda:0")
     count = (args.mib << 20) // 4
     g = torch.Generator(device=dev).manual_seed(1000 + rank)

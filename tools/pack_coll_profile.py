@@ -27,6 +27,7 @@ def main():
            "configs": {}}
     for cfg, v in s["configs"].items():
         mib, algo = cfg.split(":")
+        algo = algo.split("/")[0]  # "pullpush/0": slice-count variant
         S = int(mib) << 20
         ph = v["run"].get("phases_us_per_rank")
         r = {"device_ms_median": v["run"]["device_ms_median"],
