@@ -163,7 +163,10 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
 #define MPIGX_KNOB_SYNC_SPIN 12       /* MPIGX_SYNC_SPIN: 0/1 */
 #define MPIGX_KNOB_STAGING_BYTES 13   /* MPIGX_STAGING_BYTES (init only) */
 #define MPIGX_KNOB_LL_MAX 14          /* MPIGX_LL_MAX (init only) */
-#define MPIGX_KNOB_COUNT 15
+#define MPIGX_KNOB_AR_SLICES 15       /* MPIGX_AR_SLICES: pull-push two-shot / zero-copy Reduce slices per
+                                         block handed out dynamically (0, default: one static slice per
+                                         block; 1-64) */
+#define MPIGX_KNOB_COUNT 16
 #define MPIGX_ALGO_AUTO 0     /* unset: static rules + the measured choices */
 #define MPIGX_ALGO_LL 1       /* "ll" */
 #define MPIGX_ALGO_LL2 2      /* "ll2" */

@@ -126,6 +126,11 @@ struct PeerView {
   unsigned zc_key;             // id of the buffer-mapping view this launch uses
   int zc_bad;                  // 1: this rank has no valid view (the launch aborts everywhere)
   unsigned long long* stamps;  // diagnostic phase timestamps [block][8] (null: off)
+  // dynamic slice hand-out (ar_zc_kernel AG_PUSH, dyn): monotone counters at
+  // dcount[1] (tickets) and dcount[2] (finished blocks); their values before
+  // this launch
+  unsigned long long wbase;
+  unsigned long long fbase;
 };
 
 // Fold-kernel arguments.  Sources/partition are resolved on the host.
@@ -161,7 +166,7 @@ struct FoldArgs {
   const char* ll_in;
   long long ll_stride;
   unsigned ll_flag;    // this launch's flag (never 0, never a stale flag of the same parity)
-  int ll_pad;
+  int dyn;             // ar_zc_kernel AG_PUSH: 1 = slices of `slice` elements handed out by a ticket counter
 };
 
 // Ring reduce-scatter + allgather (MPIGX_ALGO=ring; kernels.hpp ring_kernel).

@@ -746,8 +746,9 @@ __device__ __forceinline__ void fold_span(const FoldArgs& A, const T* const* src
 }
 
 // fold_span with every folded vector stored into m outputs (outs[0..m-1]:
-// my recvbuf, then the peers' — the push-allgather two-shot, kernels.hpp
-// ar_zc_kernel AG_PUSH).  SH_FULL: m == NMAX, the stores carry no guard.
+// my recvbuf, then the peers' — the pull-push two-shot, kernels.hpp
+// ar_zc_kernel AG_PUSH; the root's recvbuf alone for Reduce).  The store
+// guards are wave-uniform and follow the loads.
 // Each element is read (all its leaves) and then written by ONE thread, so
 // in-place buffers (sendbuf == recvbuf on some rank) are safe: no other
 // thread of any rank touches that element.  `vec` false (a pointer not 16-B
@@ -763,7 +764,7 @@ __device__ __forceinline__ void fold_span_scatter(const FoldArgs& A, const T* co
     fold_at<OP, T, NMAX, SCHED, SHAPE, 1>(A, src, src2, e, r);
 #pragma unroll
     for (int p = 0; p < NMAX; ++p)
-      if (SHAPE == SH_FULL || p < m) outs[p][e] = r.x[0];
+      if (p < m) outs[p][e] = r.x[0];
   };
   if (!vec) {
     for (long long e = lo + tid; e < hi; e += nt) put1(e);
@@ -783,7 +784,7 @@ __device__ __forceinline__ void fold_span_scatter(const FoldArgs& A, const T* co
       if (fold_leaves<OP, T, NMAX, SCHED, SHAPE, W>(A, e, L[u], r)) {
 #pragma unroll
         for (int p = 0; p < NMAX; ++p)
-          if (SHAPE == SH_FULL || p < m) stv<T, W>(outs[p] + e, r);
+          if (p < m) stv<T, W>(outs[p] + e, r);
       } else {
         strad |= 1u << u;
       }
@@ -799,7 +800,7 @@ __device__ __forceinline__ void fold_span_scatter(const FoldArgs& A, const T* co
     if (fold_at<OP, T, NMAX, SCHED, SHAPE, W>(A, src, src2, e, r)) {
 #pragma unroll
       for (int p = 0; p < NMAX; ++p)
-        if (SHAPE == SH_FULL || p < m) stv<T, W>(outs[p] + e, r);
+        if (p < m) stv<T, W>(outs[p] + e, r);
     } else {
       for (int w = 0; w < W; ++w) put1(e + w);
     }
@@ -912,6 +913,63 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
 // launch whose peers STORE into this rank's memory (push two-shot).
 __device__ __forceinline__ bool rank_barrier_exit(const PeerView& pv, uint64_t ep, int* abort = nullptr) {
   return rank_barrier(pv, ep, abort, 0, false, false);
+}
+
+// Whole-launch barrier across ranks (the dynamic pull-push two-shot,
+// kernels.hpp ar_zc_kernel): every block of this rank counts itself on a
+// device counter after a system-scope release of its stores; the block that
+// completes the count (`last`) stores the rank's word into row kMaxBlocks of
+// every rank's signal array (slot [kMaxBlocks][my rank], after one more
+// release), and every block then waits until all n ranks' words reached
+// `ep` (acquire).  Counter values are monotone per communicator: base =
+// pv.fbase, this launch's blocks take base .. base + grid - 1.  The abort bit
+// travels as in rank_barrier (identical in every block of a launch).
+__device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t ep, int* abort) {
+  __shared__ int s_fail, s_abort, s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int ab_in = *abort;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this block's stores, peers' memory included
+    const unsigned long long prev =
+        __hip_atomic_fetch_add(pv.dcount + 2, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == pv.fbase + gridDim.x - 1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const size_t row = (size_t)kMaxBlocks * kMaxRanks;
+    if (s_last) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    bool ok = true, ab = false;
+    if (lane < pv.n) {
+      if (s_last) {
+        const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24);
+        __hip_atomic_store(pv.sig[lane] + row + pv.rank, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      const uint64_t* mine = pv.sig[pv.rank] + row + lane;
+      const uint64_t t0 = wall_clock64();
+      uint64_t v;
+      while (((v = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> kSigShift) < ep) {
+        __builtin_amdgcn_s_sleep(2);
+        if (wall_clock64() - t0 > pv.timeout_ticks) {
+          ok = false;
+          break;
+        }
+      }
+      ab = ok && ((v >> 24) & 1u);
+    }
+    const bool all_ok = __all(ok);
+    const bool any_ab = __any(ab);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (lane == 0) {
+      s_fail = all_ok ? 0 : 1;
+      s_abort = (ab_in || any_ab) ? 1 : 0;
+      if (!all_ok) __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __syncthreads();
+  *abort = s_abort;
+  return s_fail == 0;
 }
 
 // Zero-copy launches (mpigx.cpp zc_run): entry barrier with the view key and

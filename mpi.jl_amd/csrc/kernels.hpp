@@ -529,43 +529,78 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
     return;
   }
   stamp(pv, 1);
-  if (!ab) {
-    const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
-    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
-    bool vec = ((uintptr_t)recv & 15) == 0;
+  const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+  bool vec = ((uintptr_t)recv & 15) == 0;
 #pragma unroll
-    for (int s = 0; s < NMAX; ++s)
-      if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
-    if constexpr (SHAPE == SH_PRE) {
+  for (int s = 0; s < NMAX; ++s)
+    if (s < A.ntree) vec &= ((uintptr_t)A.src[s] & 15) == 0;
+  if constexpr (SHAPE == SH_PRE) {
 #pragma unroll
-      for (int s = 0; s < NMAX / 2; ++s)
-        if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
-    }
-    if constexpr (AG == AG_PUSH) {
-      T* outs[NMAX];  // mine first, then the peers' recvbufs
-#pragma unroll
-      for (int j = 0; j < NMAX; ++j) {
-        outs[j] = recv;
-        if (j > 0 && j < n) {
-          outs[j] = (T*)A.zc_recv[(r + j) % n];
-          vec &= ((uintptr_t)outs[j] & 15) == 0;
-        }
-      }
-      fold_span_scatter<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, hi, outs, n, vec);
-    } else {
-      if (vec) fold_span<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, hi, recv, nullptr);
-      else fold_range<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, lo, hi, recv, nullptr, false, tid, nt);
-    }
+    for (int s = 0; s < NMAX / 2; ++s)
+      if (s < A.rem) vec &= ((uintptr_t)A.src2[s] & 15) == 0;
   }
-  stamp(pv, 2);
   if constexpr (AG == AG_PUSH) {
-    stamp(pv, 3);
-    stamp(pv, 4);
-    rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
+    // Allreduce: mine first, then the peers' recvbufs; Reduce (M_RED_ZC):
+    // the root's recvbuf only
+    const bool red = A.mode == M_RED_ZC;
+    const int m = red ? 1 : n;
+    T* outs[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      outs[j] = red ? (T*)A.zc_recv[A.root] : recv;
+      if (!red && j > 0 && j < n) outs[j] = (T*)A.zc_recv[(r + j) % n];
+      if (j < m) vec &= ((uintptr_t)outs[j] & 15) == 0;
+    }
+    if (A.dyn) {
+      // slices of my chunk handed out by a ticket counter (a block that
+      // finishes early takes the next slice instead of idling until the
+      // slowest block's static share is done); every block takes tickets
+      // until one is past the end, so a launch consumes exactly
+      // slices + grid tickets (mpigx.cpp allreduce_zc advances wbase by that)
+      __shared__ long long s_tk;
+      unsigned long long* tickets = pv.dcount + 1;
+      const long long nsl = (c1 - c0 + A.slice - 1) / A.slice;
+      if (tid == 0)
+        s_tk = (long long)(__hip_atomic_fetch_add(tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - pv.wbase);
+      __syncthreads();
+      long long tk = s_tk;
+      while (tk < nsl) {
+        long long nxt = 0;  // the next ticket, taken while this slice streams
+        if (tid == 0)
+          nxt = (long long)(__hip_atomic_fetch_add(tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - pv.wbase);
+        if (!ab) {
+          const long long lo = c0 + tk * A.slice;
+          fold_span_scatter<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, lmin(lo + A.slice, c1), outs, m, vec);
+        }
+        __syncthreads();
+        if (tid == 0) s_tk = nxt;
+        __syncthreads();
+        tk = s_tk;
+      }
+      stamp(pv, 2);
+      stamp(pv, 3);
+      stamp(pv, 4);
+      rank_barrier_grid(pv, ep++, &ab);  // every rank's blocks are done: my recvbuf is complete
+    } else {
+      if (!ab) {
+        const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+        fold_span_scatter<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, hi, outs, m, vec);
+      }
+      stamp(pv, 2);
+      stamp(pv, 3);
+      stamp(pv, 4);
+      rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
+    }
     stamp(pv, 5);
     signal_done(pv, ab);
     return;
   }
+  if (!ab) {
+    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+    if (vec) fold_span<OP, T, NMAX, S_TREE, SHAPE, U>(A, src, src2, lo, hi, recv, nullptr);
+    else fold_range<OP, T, NMAX, S_TREE, SHAPE>(A, src, src2, lo, hi, recv, nullptr, false, tid, nt);
+  }
+  stamp(pv, 2);
   if (!rank_barrier(pv, ep++, &ab)) {  // every reduced chunk is in its owner's recvbuf
     signal_done(pv, 0);
     return;

@@ -266,6 +266,8 @@ PeerView make_view(mpigx_comm* c) {
   pv.done = (c->blocking && c->sync_mode == 1) ? c->done_dev : nullptr;
   pv.dcount = c->dcount_dev;
   pv.dbase = c->dcount_total;
+  pv.wbase = c->wtickets;
+  pv.fbase = c->wfinished;
   pv.seq = c->launch_seq + 1;
   pv.stamps = c->stamps;
   for (int p = 0; p < c->n; ++p) {
@@ -692,9 +694,8 @@ void zc_apply(PeerView& pv, const ZcLaunch& z) {
 // Zero-copy two-shot Allreduce over the whole message (no rounds: nothing is
 // staged).  Same chunk/slice partition and fold schedule as M_AR_TWOSHOT.
 // push_ag: the pull-push variant (ar_zc_kernel AG_PUSH: the reduce-scatter
-// stores into every rank's recvbuf); it needs the dedicated kernel and every
-// buffer 16-B aligned (the same test on every rank: the view's pointers are
-// the agreed ones), otherwise the pull two-shot runs.
+// stores into every rank's recvbuf); it needs the dedicated kernel (n <= 8,
+// MPICH tree order), otherwise the pull two-shot runs.
 int allreduce_zc(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeInfo* t, int oc, bool push_ag) {
   const int n = c->n, es = t->size;
   const int vec = es >= 16 ? 1 : 16 / es;
@@ -719,18 +720,88 @@ int allreduce_zc(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeIn
   int znmax, zshape;
   const bool dedicated =
       sched == S_TREE && c->algo != MPIGX_ALGO_PULL_GENERIC && arzc_shape(n, a.ntree, a.rem, &znmax, &zshape);
-  bool aligned = true;
-  for (int p = 0; p < n; ++p) aligned &= (((uintptr_t)z.ps[p] | (uintptr_t)z.pr[p]) & 15) == 0;
-  const int ag = (push_ag && dedicated && aligned) ? AG_PUSH : AG_PULL;
+  // (not from the pointers: a rank whose optimistic view is stale launches
+  // with null ones, and every rank must pick the same kernel; unaligned
+  // buffers take the kernels' scalar paths)
+  const int ag = (push_ag && dedicated) ? AG_PUSH : AG_PULL;
   const int grid = grid_for(c, a.chunk * es, dedicated ? cap_arzc(c, t, oc, znmax, zshape, ag)
                                                         : cap_fold(c, t, oc, nmax, sched));
   a.slice = rup(cdiv(a.chunk, grid), vec);
+  long long tickets = 0;
+  if (ag == AG_PUSH && c->ar_slices > 0) {
+    // dynamic hand-out: ar_slices slices per block (at least 32 KiB each);
+    // the kernel consumes my chunk's slices + one past-the-end ticket per block
+    a.dyn = 1;
+    a.slice = rup(cdiv(a.chunk, (long long)grid * c->ar_slices), vec);
+    const long long min_slice = rup(cdiv(32 << 10, es), vec);
+    if (a.slice < min_slice) a.slice = min_slice;
+    const long long c0 = std::min((long long)c->rank * a.chunk, count), c1 = std::min(c0 + a.chunk, count);
+    tickets = cdiv(c1 - c0, a.slice) + grid;
+  }
   if (dedicated)
     HIPCK(arzc_launcher(t->rep)(oc, znmax, zshape, ag, dim3(grid), c->stream, a));
   else
     HIPCK(fold_launcher(t->rep)(oc, nmax, sched, dim3(grid), c->stream, a));
   note_launch(c, a.pv, grid);
+  if (a.dyn) {
+    c->wtickets += tickets;
+    c->wfinished += grid;
+  }
   c->epoch += ag == AG_PUSH ? 2 : 3;
+  return MPIGX_SUCCESS;
+}
+
+// Zero-copy Reduce straight into the root's recvbuf: every rank folds its
+// chunk from every rank's sendbuf and stores it into chunk r of the root's
+// recvbuf through the view's mapping (ar_zc_kernel AG_PUSH in M_RED_ZC mode:
+// one output), dynamic slices and the whole-launch exit barrier as for the
+// pull-push Allreduce.  No arena, no rounds, no gather by the root.  Returns
+// -1 (nothing launched) where the dedicated kernel does not apply (n > 8,
+// LINEAR order, MPIGX_ALGO=pull_generic) — the caller runs the arena path
+// (M_RED_ZC in fold_kernel).
+int reduce_zc_push(mpigx_comm* c, const ZcLaunch& z, long long count, const TypeInfo* t, int oc, int root) {
+  const int n = c->n, es = t->size;
+  const int vec = es >= 16 ? 1 : 16 / es;
+  if (c->algo == MPIGX_ALGO_PULL_GENERIC) return -1;
+  FoldArgs a;
+  memset(&a, 0, sizeof a);
+  a.pv = make_view(c);
+  zc_apply(a.pv, z);
+  a.mode = M_RED_ZC;
+  a.esize = es;
+  a.count = count;
+  a.gbase = 0;
+  a.root = root;
+  a.send = z.ps[c->rank];
+  a.recv = z.pr[c->rank];
+  for (int p = 0; p < n; ++p) a.zc_recv[p] = z.pr[p];
+  int nmax, sched;
+  const void* ptrs[kMaxRanks];
+  for (int p = 0; p < n; ++p) ptrs[p] = z.ps[p];
+  plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
+  a.chunk = rup(cdiv(count, n), vec);
+  int znmax, zshape;
+  // decided from agreed settings only, never from the view's pointers (a
+  // stale optimistic view is all null on its rank; see allreduce_zc)
+  if (sched != S_TREE || !arzc_shape(n, a.ntree, a.rem, &znmax, &zshape)) return -1;
+  const int grid = grid_for(c, a.chunk * es, cap_arzc(c, t, oc, znmax, zshape, AG_PUSH));
+  a.slice = rup(cdiv(a.chunk, grid), vec);
+  long long tickets = 0;
+  if (c->ar_slices > 0) {
+    a.dyn = 1;
+    a.slice = rup(cdiv(a.chunk, (long long)grid * c->ar_slices), vec);
+    const long long min_slice = rup(cdiv(32 << 10, es), vec);
+    if (a.slice < min_slice) a.slice = min_slice;
+    const long long c0 = std::min((long long)c->rank * a.chunk, count), c1 = std::min(c0 + a.chunk, count);
+    tickets = cdiv(c1 - c0, a.slice) + grid;
+  }
+  HIPCK(arzc_launcher(t->rep)(oc, znmax, zshape, AG_PUSH, dim3(grid), c->stream, a));
+  note_launch(c, a.pv, grid);
+  if (a.dyn) {
+    c->wtickets += tickets;
+    c->wfinished += grid;
+  }
+  c->epoch += 2;
   return MPIGX_SUCCESS;
 }
 
@@ -1098,6 +1169,8 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     // (rounds of n chunks of at most one arena each) for the root to gather
     bool staged;
     const int rc = zc_run(c, send, recv ? recv : (void*)send, &staged, [&](const ZcLaunch& z) {
+      const int pr = reduce_zc_push(c, z, count, t, oc, root);
+      if (pr != -1) return pr;
       long long zround = (long long)(c->stage_bytes / es) / vec * vec * n;
       for (long long off = 0; off < count; off += zround) {
         const long long cnt = count - off < zround ? count - off : zround;
@@ -1502,7 +1575,8 @@ const char* const kAlgoNames[] = {"",     "ll",   "ll2",  "oneshot",      "twosh
 const char* const kKnobEnv[MPIGX_KNOB_COUNT] = {
     "MPIGX_ALGO",   "MPIGX_BCAST",      "MPIGX_RING_CHANNELS", "MPIGX_MAX_BLOCKS",     "MPIGX_ONESHOT_MAX",
     "MPIGX_ZC_MIN", "MPIGX_BCAST_SAG_MIN", "MPIGX_ZC_REQUIRE", "MPIGX_BYTES_PER_BLOCK", "MPIGX_LL_AUTO",
-    "MPIGX_AR_TUNE", "MPIGX_ZC_OPTIMISTIC", "MPIGX_SYNC_SPIN", "MPIGX_STAGING_BYTES",  "MPIGX_LL_MAX"};
+    "MPIGX_AR_TUNE", "MPIGX_ZC_OPTIMISTIC", "MPIGX_SYNC_SPIN", "MPIGX_STAGING_BYTES",  "MPIGX_LL_MAX",
+    "MPIGX_AR_SLICES"};
 
 long long knob_value(const mpigx_comm* c, int k) {
   switch (k) {
@@ -1521,6 +1595,7 @@ long long knob_value(const mpigx_comm* c, int k) {
     case MPIGX_KNOB_SYNC_SPIN: return c->sync_mode;
     case MPIGX_KNOB_STAGING_BYTES: return (long long)c->stage_bytes;
     case MPIGX_KNOB_LL_MAX: return c->ll_max;
+    case MPIGX_KNOB_AR_SLICES: return c->ar_slices;
     default: return -1;
   }
 }
@@ -1595,6 +1670,10 @@ int knob_apply(mpigx_comm* c, int k, long long v, bool init) {
       if (!init) return MPIGX_ERR_ARG;
       c->ll_max = v < 0 ? 0 : v > (4ll << 20) ? (4ll << 20) : v;
       return MPIGX_SUCCESS;
+    case MPIGX_KNOB_AR_SLICES:
+      if (!in(0, 64)) return MPIGX_ERR_ARG;
+      c->ar_slices = (int)v;
+      return MPIGX_SUCCESS;
     default: return MPIGX_ERR_ARG;
   }
 }
@@ -1652,6 +1731,10 @@ int knobs_from_env(mpigx_comm* c) {
   c->ar_tune = env_ll("MPIGX_AR_TUNE", 1) != 0 ? 1 : 0;
   c->zc_optimistic = env_ll("MPIGX_ZC_OPTIMISTIC", 1) != 0;
   c->sync_mode = env_ll("MPIGX_SYNC_SPIN", 1) != 0 ? 1 : 0;
+  // static slices by default: on ranks sharing one GPU the ticket hand-out
+  // moved the straggler tail but not the span (profiles/r03e_coll_n2_1gpu.json)
+  const long long sl = env_ll("MPIGX_AR_SLICES", 0);
+  c->ar_slices = (int)(sl < 0 ? 0 : sl > 64 ? 64 : sl);
   return MPIGX_SUCCESS;
 }
 
@@ -1698,7 +1781,9 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   c->test_import_fail = (int)env_ll("MPIGX_TEST_IMPORT_FAIL", 0);  // per rank: fault injection, not a knob
 
   HIPCK(hipMalloc(&c->stage, c->stage_bytes));
-  const size_t sig_bytes = (size_t)kMaxBlocks * kMaxRanks * sizeof(uint64_t);
+  // rows [0, kMaxBlocks): per-block barriers; row kMaxBlocks: whole-launch
+  // barrier (device.hpp rank_barrier_grid)
+  const size_t sig_bytes = (size_t)(kMaxBlocks + 1) * kMaxRanks * sizeof(uint64_t);
   HIPCK(hipExtMallocWithFlags((void**)&c->sig, sig_bytes, hipDeviceMallocUncached));
   HIPCK(hipMemset(c->sig, 0, sig_bytes));
   // LL area for small messages (M_AR_LL ...): uncached like the signal array,

@@ -15,7 +15,7 @@ namespace mpigx {
 // ---------------------------------------------------------------------------
 // shm block (one per communicator, mapped by every rank)
 // ---------------------------------------------------------------------------
-constexpr uint64_t kMagic = 0x6d70696778763033ull;  // "mpigxv03"
+constexpr uint64_t kMagic = 0x6d70696778763034ull;  // "mpigxv04"
 
 struct ShmRank {
   int pid;
@@ -141,6 +141,10 @@ struct mpigx_comm {
   int ar_tune = 1;                // MPIGX_AR_TUNE
   int ar_step = 0;                // zero-copy Allreduces seen while undecided
   double ar_spb[3] = {0, 0, 0};   // device seconds per byte: pull, push, pull-push (this rank)
+  int ar_slices = 0;              // MPIGX_AR_SLICES: dynamic pull-push slices per block (0: static)
+  // dynamic slice hand-out counters (dcount_dev[1] tickets, [2] finished
+  // blocks): totals of every launch so far, the next launch's bases
+  unsigned long long wtickets = 0, wfinished = 0;
   hipEvent_t ar_ev[2] = {nullptr, nullptr};
   // small / medium Allreduce tuner (mpigx.cpp mt_*): per size class
   // (floor(log2 bytes)) the measured choice among LL / one-shot / two-shot

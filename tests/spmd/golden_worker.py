@@ -386,6 +386,37 @@ class Runner:
                 assert L.mpigx_comm_tune_class(cv, k + 64 * kind, ctypes.byref(ch), None) == 0
                 self.check(ch.value in (0, 1), ("tune-decided-copy", kind, k, ch.value))
 
+    def unaligned_cases(self):
+        """Zero-copy Allreduce / Reduce on buffers 4 B past a 16-B boundary
+        (the dedicated kernels' scalar paths; the kernel choice never looks
+        at the pointers), every algorithm, IN_PLACE too, vs the oracle."""
+        L, n, r, cv = self.L, self.n, self.r, self.comm.val
+        count = 100_003
+        ins = make("FLOAT", "SUM", n, count, 4700)
+        exp = M.allreduce(ins, "FLOAT", "SUM")[r]
+        h, op = M.DTYPES["FLOAT"][0], M.OPS["SUM"]
+        for algo in ("pull", "pullpush", "pull_generic", "push", None):
+            self.knob("ALGO", algo)
+            for inplace in (False, True):
+                sraw = dev(np.concatenate([np.zeros(1, np.float32), ins[r]]))
+                rraw = dev(np.zeros(count + 1, np.float32)) if not inplace else sraw
+                s = ctypes.c_void_p(sraw.data_ptr() + 4)
+                d = ctypes.c_void_p(rraw.data_ptr() + 4)
+                rc = L.mpigx_allreduce(IN_PLACE if inplace else s, d, count, h, op, cv)
+                self.check(rc == 0, ("unaligned allreduce rc", algo, inplace))
+                got = host(rraw, np.float32)[1:]
+                self.check(same_bits(got, exp), ("unaligned allreduce", algo, inplace))
+            root = (n - 1) if algo else 0
+            sraw = dev(np.concatenate([np.zeros(1, np.float32), ins[r]]))
+            rraw = dev(np.zeros(count + 1, np.float32))
+            rc = L.mpigx_reduce(ctypes.c_void_p(sraw.data_ptr() + 4), ctypes.c_void_p(rraw.data_ptr() + 4), count, h,
+                                op, root, cv)
+            self.check(rc == 0, ("unaligned reduce rc", algo))
+            if r == root:
+                self.check(same_bits(host(rraw, np.float32)[1:], M.reduce(ins, "FLOAT", "SUM", root)),
+                           ("unaligned reduce", algo))
+        self.knob("ALGO", None)
+
     def ring_cases(self, nchs=(1, 2, 4)):
         """MPIGX_ALGO=ring (zero-copy path): bit-exact against the ring's own
         association (oracle fold_ring, rounds included), and against MPICH:
@@ -456,6 +487,7 @@ def main():
     zc = bool(os.environ.get("MPIGX_ZC_MIN"))
     if zc:
         R.ring_cases()
+        R.unaligned_cases()
     if phase == "all":
         # rounds: a communicator whose staging arena is 1 MiB forces multi-round launches
         os.environ["MPIGX_STAGING_BYTES"] = str(1 << 20)

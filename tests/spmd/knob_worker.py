@@ -87,7 +87,7 @@ def main():
                 except MPI.MPIError:
                     pass
             MPI.set_knob(comm, "ZC_MIN", 1)
-            for algo in ("ring", "push", "pull", "pull_generic", "oneshot", "twoshot", "ll", None):
+            for algo in ("ring", "push", "pull", "pull_generic", "pullpush", "oneshot", "twoshot", "ll", None):
                 MPI.set_knob(comm, "ALGO", algo)
                 if MPI.get_knob(comm, "ALGO") != MPI.ALGOS[algo]:
                     fails.append(("get_knob", algo))
@@ -96,6 +96,28 @@ def main():
                 MPI.Allreduce_(dev(ins[r]), recv, MPI.SUM, comm)
                 if not same_bits(recv.cpu().numpy(), M.allreduce(ins, "INT32_T", "SUM")[r]):
                     fails.append(("result", algo))
+            # the pull-push two-shot's dynamic slice hand-out: ticket counters
+            # carry over launches (monotone bases), across slice counts, the
+            # static variant and other algorithms in between
+            MPI.set_knob(comm, "ALGO", "pullpush")
+            for count in (50_001, (3 << 20) + 5):
+                ins = make("FLOAT", "SUM", n, count, 41)
+                exp = M.allreduce(ins, "FLOAT", "SUM")[r]
+                src = dev(ins[r])
+                for slices in (0, 1, 7, 64, 4, 0, 4):
+                    MPI.set_knob(comm, "AR_SLICES", slices)
+                    if MPI.get_knob(comm, "AR_SLICES") != slices:
+                        fails.append(("AR_SLICES knob", slices))
+                    for _ in range(2):
+                        recv = torch.zeros(count, dtype=torch.float32, device="cuda")
+                        MPI.Allreduce_(src, recv, MPI.SUM, comm)
+                        if not same_bits(recv.cpu().numpy(), exp):
+                            fails.append(("pullpush slices", count, slices))
+                    MPI.set_knob(comm, "ALGO", "pull")
+                    MPI.Allreduce_(src, recv, MPI.SUM, comm)
+                    MPI.set_knob(comm, "ALGO", "pullpush")
+            MPI.set_knob(comm, "AR_SLICES", 0)
+            MPI.set_knob(comm, "ALGO", None)
             MPI.set_knob(comm, "ZC_MIN", 16 << 20)
         elif sc == "share":
             ranks, cap = MPI.device_share(comm)
