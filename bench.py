@@ -567,6 +567,14 @@ def bench_allreduce(args):
                 buf = torch.full((cnt,), float(rank), device=dev)
                 tb = time_call(lambda: MPI.Bcast_(buf, 0, comm), steps, 2, 6)
                 okb = bool(torch.all(buf == 0).item())
+                tbs = None
+                if nb >= (128 << 20) and n >= 3:
+                    # the pull scatter + allgather the zero-copy relay replaced
+                    MPI.set_knob(comm, "BCAST", "sag")
+                    buf.fill_(float(rank))
+                    tbs = time_call(lambda: MPI.Bcast_(buf, 0, comm), steps, 1)
+                    okb &= bool(torch.all(buf == 0).item())
+                    MPI.set_knob(comm, "BCAST", None)
                 per = cnt // n
                 src = torch.full((per,), float(rank), device=dev)
                 dst = torch.empty(per * n, device=dev)
@@ -582,6 +590,8 @@ def bench_allreduce(args):
                 cfg4[f"{nb >> 10}KiB"] = {
                     "bcast_busbw": round(nb / tb / 1e9, 2), "allgather_busbw": round(nb / tg / 1e9 * f, 2),
                     "alltoall_busbw": round(nb / ta / 1e9 * f, 2), "ok": bad == 0.0}
+                if tbs:
+                    cfg4[f"{nb >> 10}KiB"]["bcast_sag_busbw"] = round(nb / tbs / 1e9, 2)
                 del buf, src, dst, a2s, a2r
     guarded("config4", config4_section)
     # the byte movers' tuner at config 4's smallest sizes (per-rank block)

@@ -149,7 +149,7 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
  * nothing, when they differ.  The two init-only knobs (allocation sizes)
  * cannot be set. */
 #define MPIGX_KNOB_ALGO 0             /* MPIGX_ALGO: MPIGX_ALGO_* below */
-#define MPIGX_KNOB_BCAST 1            /* MPIGX_BCAST: 0 auto, 1 "direct", 2 "sag" */
+#define MPIGX_KNOB_BCAST 1            /* MPIGX_BCAST: 0 auto, 1 "direct", 2 "sag", 3 "relay" */
 #define MPIGX_KNOB_RING_CHANNELS 2    /* MPIGX_RING_CHANNELS: rings of MPIGX_ALGO_RING (1-4) */
 #define MPIGX_KNOB_MAX_BLOCKS 3       /* MPIGX_MAX_BLOCKS: grid cap of the collective kernels */
 #define MPIGX_KNOB_ONESHOT_MAX 4      /* MPIGX_ONESHOT_MAX: bytes */

@@ -106,7 +106,11 @@ enum CopyMode : int {
   // when it has nothing to send (Bcast non-roots), so every rank receives from
   // every rank and the area parities stay safe — and unpacks what it needs
   // straight into the user buffer
-  C_BCAST_LL = 11, C_ALLGATHER_LL = 12, C_ALLTOALL_LL = 13
+  C_BCAST_LL = 11, C_ALLGATHER_LL = 12, C_ALLTOALL_LL = 13,
+  // zero-copy relay (large, n >= 3): the non-roots own the n - 1 chunks; the
+  // owner of chunk i reads it from the root's buffer once and stores it into
+  // its own and every other non-root's buffer in the same pass
+  C_BCAST_RELAY_ZC = 14
 };
 
 // Per-call view of the communicator, passed by value to every kernel.
@@ -167,6 +171,7 @@ struct FoldArgs {
   long long ll_stride;
   unsigned ll_flag;    // this launch's flag (never 0, never a stale flag of the same parity)
   int dyn;             // ar_zc_kernel AG_PUSH: 1 = slices of `slice` elements handed out by a ticket counter
+  int own;             // M_RED_ZC (ar_zc_kernel): index of the chunk this rank folds (root: none at n >= 3)
 };
 
 // Ring reduce-scatter + allgather (MPIGX_ALGO=ring; kernels.hpp ring_kernel).
@@ -290,7 +295,9 @@ struct ScanArgs {
   long long ll_stride;
   long long ll_ustride;
   unsigned ll_flag;
-  int ll_pad;
+  int pp;              // 1: pull-push zero-copy (n <= 8): rank r computes EVERY rank's result for chunk r
+  long long chunk;     // pp: elements per rank chunk (multiple of vec)
+  char* zrecv[kMaxRanks];  // pp: every rank's recvbuf (zero-copy view)
 };
 
 }  // namespace mpigx

@@ -43,6 +43,50 @@ __device__ __forceinline__ void block_copy_u(char* dst, const char* src, long lo
   block_gather_u<1, U>(d, s, l, 1);
 }
 
+// one source -> up to NMAX destinations (null = none): every 16-B vector is
+// loaded once (U per thread in flight, unguarded: a lane past the end
+// re-reads the last vector) and stored to each destination; unaligned
+// operands go byte by byte
+// (the pointers come from LDS: made wave-uniform, device.hpp wave_uniform)
+template <int NMAX, int U>
+__device__ __forceinline__ void block_relay_u(char* const (&outs)[NMAX], const char* src, long long len) {
+  if (len <= 0) return;
+  const long long tid = threadIdx.x, nt = blockDim.x;
+  src = wave_uniform(src);
+  char* o[NMAX];
+  bool vec = ((uintptr_t)src & 15) == 0;
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) {
+    o[j] = wave_uniform(outs[j]);
+    if (o[j]) vec &= ((uintptr_t)o[j] & 15) == 0;
+  }
+  long long done = 0;
+  if (vec) {
+    const long long nv = len / 16;
+    for (long long i = tid; i < nv; i += U * nt) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long k = i + u * nt;
+        v[u] = ld16(src + 16 * (k < nv ? k : nv - 1));
+      }
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j)
+        if (o[j])
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (i + u * nt < nv) st16(o[j] + 16 * (i + u * nt), v[u]);
+    }
+    done = nv * 16;
+  }
+  for (long long k = done + tid; k < len; k += nt) {
+    const char c = src[k];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j)
+      if (o[j]) o[j][k] = c;
+  }
+}
+
 template <int NMAX, int U>
 __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the zero-copy abort verdict
   const PeerView& pv = A.pv;
@@ -219,6 +263,30 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     if (!zc_enter(pv, ep++, &ab)) return 0;
     if (!ab && r != A.root) block_copy_u<2 * U>(recv + lo, A.zsrc[A.root] + lo, len);
     rank_barrier_exit(pv, ep++, &ab);
+    return ab;
+  }
+  if (A.mode == C_BCAST_RELAY_ZC) {
+    // relay: the n - 1 non-roots own the n - 1 chunks (owner i = root + 1 + i);
+    // the owner pulls slice b of its chunk from the root's buffer and stores
+    // it into its own buffer and every other non-root's (their mappings) in
+    // the same pass.  Root links carry S/(n-1) out, every link between
+    // non-roots S/(n-1) each way: one pass and one barrier fewer than the
+    // scatter + allgather, whose root links carry 2S/n in two phases.  The
+    // exit barrier is the fenced one: it publishes the stores into peers.
+    long long l, h;
+    int ab;
+    if (!zc_enter(pv, ep++, &ab)) return 0;
+    if (!ab && r != A.root) {
+      chunk_slice(A, (r - A.root - 1 + n) % n, b, &l, &h);
+      char* outs[NMAX];
+#pragma unroll
+      for (int j = 0; j < NMAX; ++j) {
+        const int p = (r + j) % n;
+        outs[j] = (j < n && p != A.root) ? (j == 0 ? recv : (char*)A.zsrc[p]) + l : nullptr;
+      }
+      block_relay_u<NMAX, NMAX <= 4 ? 8 : 4>(outs, A.zsrc[A.root] + l, h - l);
+    }
+    rank_barrier(pv, ep++, &ab);
     return ab;
   }
   if (A.mode == C_BCAST_SAG_ZC) {

@@ -533,6 +533,17 @@ __device__ __forceinline__ void fold_range(const FoldArgs& A, const T* const* sr
   for (long long e = lo + tid; e < hi; e += nthr) fold_elems<OP, T, NMAX, SCHED, SHAPE>(A, src, src2, e, 1, out1, out2);
 }
 
+// A pointer every lane of the wave holds the same value of, read from LDS
+// (the kernels stage their argument blocks there): the compiler cannot prove
+// it uniform and keeps a 64-bit address per lane per use (and waterfall
+// loops around buffer descriptors); readfirstlane puts it in SGPRs.
+template <class P>
+__device__ __forceinline__ P* wave_uniform(P* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  return (P*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
+}
+
 // ---------------------------------------------------------------------------
 // block-cooperative byte copy (alignment-peeling, 16-B vectors when possible)
 // ---------------------------------------------------------------------------

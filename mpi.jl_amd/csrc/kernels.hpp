@@ -529,7 +529,10 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
     return;
   }
   stamp(pv, 1);
-  const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+  // my chunk: chunk r, except for the zero-copy Reduce, whose chunks belong
+  // to the non-roots at n >= 3 (host reduce_zc_push)
+  const int own = A.mode == M_RED_ZC ? A.own : r;
+  const long long c0 = lmin((long long)own * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
   bool vec = ((uintptr_t)recv & 15) == 0;
 #pragma unroll
   for (int s = 0; s < NMAX; ++s)
@@ -819,6 +822,145 @@ __device__ __forceinline__ void scan_at(const ScanArgs& A, long long e, Vec<T, W
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pull-push Scan / Exscan (zero-copy, n <= 8; ScanArgs.pp).  The staged and
+// old zero-copy schedules have rank q read the contributions of ranks 0..q:
+// sum over q of (q+1) S bytes of reads (36 S at n = 8), and the top rank
+// pulls S from each of 7 peers over 7 links while rank 1 pulls from one.
+// Here the message is cut into n chunks like the two-shot Allreduce and rank
+// r owns chunk r for EVERY rank: it loads chunk r of all contributions once
+// (leaves in registers) and stores rank q's prefix of it into rank q's
+// recvbuf (peers' through the view), so every rank reads S and writes S and
+// every link carries S/n each way: n S reads instead of n(n+1)/2 S.  The
+// association per rank is the recursive-doubling one of scan_at above with
+// compile-time leaf indices (identical bits).  In place is safe: element e is
+// read (all leaves) and then written by one thread of its owner only.
+// ---------------------------------------------------------------------------
+template <class OP, class T, int W, int SIZE, int BASE, int OWNER>
+__device__ __forceinline__ void blk_total_reg(const Vec<T, W>* x, Vec<T, W>& out) {
+  if constexpr (SIZE == 1) {
+    out = x[BASE];
+  } else {
+    constexpr int H = SIZE / 2;
+    constexpr bool hi_own = ((OWNER - BASE) & H) != 0;
+    Vec<T, W> a, c;
+    blk_total_reg<OP, T, W, H, BASE, hi_own ? (OWNER ^ H) : OWNER>(x, a);       // low half
+    blk_total_reg<OP, T, W, H, BASE + H, hi_own ? OWNER : (OWNER ^ H)>(x, c);   // high half
+    if constexpr (hi_own) vapply<OP, T, W>(out, c, a);
+    else vapply<OP, T, W>(out, a, c);
+  }
+}
+
+// rank Q's result from leaves x[0..Q]: set bits M of Q in increasing order
+template <class OP, class T, int W, int Q, int M, bool HAVE>
+__device__ __forceinline__ void scan_reg_bits(const Vec<T, W>* x, Vec<T, W>& res) {
+  if constexpr (M <= Q) {
+    if constexpr ((Q & M) != 0) {
+      constexpr int D = Q ^ M;
+      Vec<T, W> t;
+      blk_total_reg<OP, T, W, M, (D & ~(M - 1)), D>(x, t);
+      if constexpr (HAVE) vapply<OP, T, W>(res, res, t);
+      else res = t;
+      scan_reg_bits<OP, T, W, Q, M * 2, true>(x, res);
+    } else {
+      scan_reg_bits<OP, T, W, Q, M * 2, HAVE>(x, res);
+    }
+  }
+}
+
+template <class OP, class T, int W, int Q, bool EXCL>
+__device__ __forceinline__ void scan_reg(const Vec<T, W>* x, Vec<T, W>& res) {
+  if constexpr (!EXCL) res = x[Q];
+  scan_reg_bits<OP, T, W, Q, 1, !EXCL>(x, res);
+}
+
+// every rank's result at vector/element e of my chunk -> rank q's recvbuf
+template <class OP, class T, int W, bool EXCL, int Q = 0>
+__device__ __forceinline__ void scan_pp_store(const ScanArgs& A, const Vec<T, W>* x, long long e) {
+  if constexpr (Q < 8) {
+    if (Q < A.pv.n) {
+      if constexpr (!(EXCL && Q == 0)) {
+        Vec<T, W> r;
+        scan_reg<OP, T, W, Q, EXCL>(x, r);
+        stv<T, W>(wave_uniform((T*)A.zrecv[Q]) + e, r);
+      }
+      scan_pp_store<OP, T, W, EXCL, Q + 1>(A, x, e);
+    }
+  }
+}
+
+// [lo, hi) of my chunk.  Vector path: U 16-B vectors per thread, all 8 x U
+// leaf loads issued before any arithmetic as buffer loads whose descriptor
+// has no records for an absent leaf (rank >= n, or the top rank's own data in
+// Exscan): such a load returns zeros without touching memory, so no branch
+// sits between the loads.  Unaligned operands and the ragged tail go element
+// by element.
+template <class OP, class T, bool EXCL, int U>
+__device__ __forceinline__ void scan_pp_span(const ScanArgs& A, long long lo, long long hi) {
+  constexpr int W = VecW<T>::v;
+  const int n = A.pv.n, nl = EXCL ? n - 1 : n;
+  const long long tid = threadIdx.x, nt = blockDim.x, es = A.esize;
+  bool vec = true;
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    if (s < n) vec &= ((((uintptr_t)A.src[s]) | ((uintptr_t)A.zrecv[s])) & 15) == 0;
+  long long e0 = lo;
+  if (vec) {
+    // descriptors cover at most 1 GiB (32-bit offsets), rebuilt per piece
+    constexpr long long kPiece = (1ll << 30) / 16;
+    const long long nv_all = (hi - lo) / W;
+    for (long long p0 = 0; p0 < nv_all; p0 += kPiece) {
+      const long long nv = lmin(nv_all - p0, kPiece), base = lo + p0 * W;
+      // descriptors from wave-uniform values (read from LDS, the compiler
+      // cannot prove them uniform and would wrap every load in a waterfall loop)
+      __amdgpu_buffer_rsrc_t rs[8];
+      const int bytes = __builtin_amdgcn_readfirstlane((int)(nv * 16));
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        rs[s] = __builtin_amdgcn_make_buffer_rsrc((void*)wave_uniform(s < nl ? A.src[s] + base * es : A.src[0]), 0,
+                                                  s < nl ? bytes : 0, 0x00020000);
+      for (long long v0 = tid; v0 < nv; v0 += U * nt) {
+        Vec<T, W> x[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int s = 0; s < 8; ++s)
+            *reinterpret_cast<u32x4*>(x[u][s].x) =
+                __builtin_amdgcn_raw_buffer_load_b128(rs[s], (int)((v0 + u * nt) * 16), 0, MPIGX_NT ? 2 : 0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (v0 + u * nt < nv) scan_pp_store<OP, T, W, EXCL>(A, x[u], base + (v0 + u * nt) * W);
+      }
+    }
+    e0 = lo + nv_all * W;
+  }
+  for (long long e = e0 + tid; e < hi; e += nt) {
+    Vec<T, 1> x[8] = {};
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s < nl) x[s].x[0] = ((const T*)A.src[s])[e];
+    scan_pp_store<OP, T, 1, EXCL>(A, x, e);
+  }
+}
+
+template <class OP, class T>
+__device__ __forceinline__ int scan_pp_body(const ScanArgs& A) {
+  const PeerView& pv = A.pv;
+  const int b = blockIdx.x, r = pv.rank;
+  uint64_t ep = pv.epoch;
+  int ab;
+  if (!zc_enter(pv, ep++, &ab)) return 0;  // every rank's buffers ready, one view
+  if (!ab) {
+    const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
+    const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
+    constexpr int U = vec_regs<T>() <= 4 ? 2 : 1;
+    if (A.exclusive) scan_pp_span<OP, T, true, U>(A, lo, hi);
+    else scan_pp_span<OP, T, false, U>(A, lo, hi);
+  }
+  rank_barrier(pv, ep++, &ab);  // publishes my stores into the peers' recvbufs
+  return ab;
+}
+
 template <class OP, class T>
 __device__ __forceinline__ int scan_body(const ScanArgs& A);
 
@@ -833,7 +975,7 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(ScanArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
-  const int ab = scan_body<OP, T>(sA);
+  const int ab = sA.pp ? scan_pp_body<OP, T>(sA) : scan_body<OP, T>(sA);
   signal_done(sA.pv, ab);
 }
 

@@ -279,6 +279,11 @@ PeerView make_view(mpigx_comm* c) {
 
 // Account for one launch of `grid` blocks made with view `pv`.
 void note_launch(mpigx_comm* c, const PeerView& pv, unsigned grid) {
+  static const bool diag = getenv("MPIGX_DIAG_TRACE") != nullptr;  // DIAG (temporary)
+  if (diag)
+    fprintf(stderr, "[trace r%d] launch epoch=%llu grid=%u key=%u bad=%d dbase=%llu seq=%llu\n", c->rank,
+            (unsigned long long)pv.epoch, grid, pv.zc_key, pv.zc_bad, (unsigned long long)pv.dbase,
+            (unsigned long long)pv.seq);
   if (c->launch_pending) {
     c->last_prelaunch_s = now_s() - c->t_entry;
     c->launch_pending = false;
@@ -341,9 +346,21 @@ int finish(mpigx_comm* c) {
 // of 256 threads, MI355X_MICROARCH.md "Residency"): one fewer there;
 // VGPR-bound counts (<= 5) are exact.  The same on every rank (same kernel,
 // agreed cus_min / dev_share).
+// Ranks sharing a device (the 1-GPU test box) never fill it: every rank's
+// grids at exactly the occupancy limit (e.g. 4 x 256 blocks of a 126-VGPR
+// kernel at n = 4) timed out in one run of three, all ranks launching the
+// same grid at the same epoch within a millisecond (tools/scan_repro.py,
+// DESIGN §3 "Ranks sharing a GPU") — some blocks of some rank never became
+// resident while the others spun.  So at most occupancy - 1 blocks per CU
+// in total there (three quarters of the CUs at occupancy 1).  One rank per
+// GPU is unaffected (its 256-block grid is at most one block per CU).
 int kernel_cap(mpigx_comm* c, int occ) {
-  const long long o = occ >= 6 ? occ - 1 : occ > 0 ? occ : 1;
-  const long long cap = (long long)c->cus_min * o / (c->dev_share > 0 ? c->dev_share : 1);
+  const long long share = c->dev_share > 0 ? c->dev_share : 1;
+  long long cap;
+  if (share > 1)
+    cap = occ >= 2 ? (long long)c->cus_min * (occ - 1) / share : (long long)c->cus_min * 3 / (4 * share);
+  else
+    cap = (long long)c->cus_min * (occ >= 6 ? occ - 1 : occ > 0 ? occ : 1);
   return (int)(cap < 1 ? 1 : cap > kMaxBlocks ? kMaxBlocks : cap);
 }
 int cap_fold(mpigx_comm* c, const TypeInfo* t, int oc, int nmax, int sched) {
@@ -779,7 +796,15 @@ int reduce_zc_push(mpigx_comm* c, const ZcLaunch& z, long long count, const Type
   const void* ptrs[kMaxRanks];
   for (int p = 0; p < n; ++p) ptrs[p] = z.ps[p];
   plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
-  a.chunk = rup(cdiv(count, n), vec);
+  // chunks: at n >= 3 only the non-roots own one (n - 1 chunks, root + 1 + i
+  // owns chunk i).  With a chunk of its own the root's incoming links carry
+  // its peers' pushes AND its own pulls (2S/n each); without, S/(n - 1): at
+  // n = 8 S/4 -> S/7 per root link.  At n = 2 the split stays (S per link
+  // direction either way, and both ranks' blocks share the work).
+  const bool xroot = n >= 3 && !getenv("MPIGX_DIAG_RED_ALL_OWN");  // DIAG (temporary)
+  const int owners = xroot ? n - 1 : n;
+  a.own = xroot ? (c->rank == root ? n - 1 : (c->rank - root - 1 + n) % n) : c->rank;
+  a.chunk = rup(cdiv(count, owners), vec);
   int znmax, zshape;
   // decided from agreed settings only, never from the view's pointers (a
   // stale optimistic view is all null on its rank; see allreduce_zc)
@@ -792,7 +817,7 @@ int reduce_zc_push(mpigx_comm* c, const ZcLaunch& z, long long count, const Type
     a.slice = rup(cdiv(a.chunk, (long long)grid * c->ar_slices), vec);
     const long long min_slice = rup(cdiv(32 << 10, es), vec);
     if (a.slice < min_slice) a.slice = min_slice;
-    const long long c0 = std::min((long long)c->rank * a.chunk, count), c1 = std::min(c0 + a.chunk, count);
+    const long long c0 = std::min((long long)a.own * a.chunk, count), c1 = std::min(c0 + a.chunk, count);
     tickets = cdiv(c1 - c0, a.slice) + grid;
   }
   HIPCK(arzc_launcher(t->rep)(oc, znmax, zshape, AG_PUSH, dim3(grid), c->stream, a));
@@ -1610,7 +1635,7 @@ int knob_apply(mpigx_comm* c, int k, long long v, bool init) {
       c->algo = (int)v;
       return MPIGX_SUCCESS;
     case MPIGX_KNOB_BCAST:
-      if (!in(0, 2)) return MPIGX_ERR_ARG;
+      if (!in(0, 3)) return MPIGX_ERR_ARG;
       c->bcast_mode = (int)v;
       return MPIGX_SUCCESS;
     case MPIGX_KNOB_RING_CHANNELS:
@@ -1699,8 +1724,9 @@ int knobs_from_env(mpigx_comm* c) {
   if (bc && *bc) {
     if (!strcmp(bc, "direct")) c->bcast_mode = 1;
     else if (!strcmp(bc, "sag")) c->bcast_mode = 2;
+    else if (!strcmp(bc, "relay")) c->bcast_mode = 3;
     else {
-      fprintf(stderr, "[mpigx] MPIGX_BCAST=%s: expected direct or sag\n", bc);
+      fprintf(stderr, "[mpigx] MPIGX_BCAST=%s: expected direct, sag or relay\n", bc);
       return MPIGX_ERR_ARG;
     }
   }
@@ -2226,10 +2252,13 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
   // direct pull from the root (one barrier less) for small messages or two
   // ranks; scatter + allgather when the root's links would be the bottleneck.
   // The choice depends only on (bytes, n, env), identical on every rank.
-  const bool env = c->bcast_mode != 0;  // MPIGX_BCAST knob: 1 direct, 2 sag
+  const bool env = c->bcast_mode != 0;  // MPIGX_BCAST knob: 1 direct, 2 sag, 3 relay
   bool sag = c->n >= 3 && bytes >= c->bcast_sag_min;
   if (c->bcast_mode == 1) sag = false;
-  if (c->bcast_mode == 2) sag = c->n >= 2;
+  if (c->bcast_mode >= 2) sag = c->n >= 2;
+  // zero-copy: the relay replaces the pull scatter + allgather (n >= 3)
+  // unless "sag" is asked for by name
+  const bool relay = sag && c->n >= 3 && c->bcast_mode != 2;
   // (zero-copy first when the size asks for it: tests force it at every size)
   // below the zero-copy size: LL or the staged copy, measured (mt_*)
   const bool zc_size = c->zc_min > 0 && bytes >= c->zc_min;
@@ -2255,8 +2284,9 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
     return mt_finish(c, timed, cls, bytes);
   }
   if (c->zc_min > 0 && bytes >= c->zc_min) {
-    // zero-copy: the non-roots pull straight from the root's buffer (and, for
-    // scatter + allgather, from each other's), no copy-in at the root
+    // zero-copy: the non-roots pull straight from the root's buffer, no
+    // copy-in at the root; large (n >= 3): the relay, each non-root pulling
+    // its chunk once and storing it into every non-root's buffer
     bool staged;
     const int rc = zc_run(c, buf, buf, &staged, [&](const ZcLaunch& z) {
       CopyArgs a;
@@ -2268,7 +2298,12 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
       a.recv = buf;
       for (int p = 0; p < c->n; ++p) a.zsrc[p] = z.ps[p];
       int g;
-      if (sag) {
+      if (relay) {
+        a.mode = C_BCAST_RELAY_ZC;
+        a.chunk = rup(cdiv(bytes, c->n - 1), 16);
+        g = grid_for(c, a.chunk, cap_copy(c));
+        a.slice = rup(cdiv(a.chunk, g), 16);
+      } else if (sag) {
         a.mode = C_BCAST_SAG_ZC;
         a.chunk = rup(cdiv(bytes, c->n), 16);
         g = grid_for(c, a.chunk, cap_copy(c));
@@ -2280,7 +2315,7 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
       }
       HIPCK(launch_copy(dim3(g), c->stream, a));
       note_launch(c, a.pv, g);
-      c->epoch += sag ? 3 : 2;
+      c->epoch += (sag && !relay) ? 3 : 2;
       return MPIGX_SUCCESS;
     });
     if (rc || !staged) return rc;
@@ -3013,9 +3048,14 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
   }
   ScanLauncher L = scan_launcher(t->rep);
   const int vec = es >= 16 ? 1 : 16 / es;
-  if (sendbuf != MPIGX_IN_PLACE && c->zc_min > 0 && (long long)count * es >= c->zc_min) {
-    // zero-copy (out of place: with IN_PLACE my recvbuf, which I overwrite,
-    // would be the operand the higher ranks read): no copy-in, no rounds
+  // pull-push (n <= 8): rank r computes every rank's result for chunk r
+  // (kernels.hpp scan_pp_body) — in place too, since each element is read
+  // and written by one thread of its owner only; n > 8 keeps the pull
+  // schedule, out of place (with IN_PLACE my recvbuf, which I overwrite,
+  // would be the operand the higher ranks read)
+  const bool pp = c->n <= 8 && !getenv("MPIGX_DIAG_NO_SCAN_PP");  // DIAG (temporary)
+  if ((pp || sendbuf != MPIGX_IN_PLACE) && c->zc_min > 0 && (long long)count * es >= c->zc_min) {
+    // zero-copy: no copy-in, no rounds
     bool staged;
     const int rc = zc_run(c, s, recvbuf, &staged, [&](const ZcLaunch& z) {
       ScanArgs a;
@@ -3026,8 +3066,17 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
       a.exclusive = exclusive;
       a.esize = es;
       a.count = count;
-      const int g = grid_for(c, (long long)count * es, cap_scan(c, t, oc));
-      a.slice = rup(cdiv(count, g), vec);
+      int g;
+      if (pp) {
+        a.pp = 1;
+        a.chunk = rup(cdiv(count, c->n), vec);
+        g = grid_for(c, a.chunk * es, cap_scan(c, t, oc));
+        a.slice = rup(cdiv(a.chunk, g), vec);
+        for (int p = 0; p < c->n; ++p) a.zrecv[p] = z.pr[p];
+      } else {
+        g = grid_for(c, (long long)count * es, cap_scan(c, t, oc));
+        a.slice = rup(cdiv(count, g), vec);
+      }
       a.send = s;
       a.recv = recvbuf;
       for (int p = 0; p < c->n; ++p) a.src[p] = z.ps[p];

@@ -561,7 +561,7 @@ KNOBS = {"ALGO": 0, "BCAST": 1, "RING_CHANNELS": 2, "MAX_BLOCKS": 3, "ONESHOT_MA
          "ZC_OPTIMISTIC": 11, "SYNC_SPIN": 12, "STAGING_BYTES": 13, "LL_MAX": 14, "AR_SLICES": 15}
 ALGOS = {None: 0, "": 0, "auto": 0, "ll": 1, "ll2": 2, "oneshot": 3, "twoshot": 4, "push": 5, "ring": 6,
          "pull": 7, "pull_generic": 8, "pullpush": 9}
-BCAST_MODES = {None: 0, "": 0, "auto": 0, "direct": 1, "sag": 2}
+BCAST_MODES = {None: 0, "": 0, "auto": 0, "direct": 1, "sag": 2, "relay": 3}
 
 
 def _knob_id(knob):

@@ -261,7 +261,7 @@ class Runner:
             ins1 = [x[:count] for x in ins]
             got = self.run("allgather", ins1, "FLOAT", None, count)
             self.check(same_bits(got, M.allgather(ins1)[r]), ("allgather", count))
-            for algo in ("direct", "sag"):  # root pull vs scatter+allgather
+            for algo in ("direct", "sag", "relay"):  # root pull vs scatter+allgather vs relay (zero-copy)
                 self.knob("BCAST", algo)
                 for root in sorted({0, n // 2, n - 1}):
                     got = self.run("bcast", ins1, "FLOAT", None, count, root=root)
@@ -330,10 +330,13 @@ class Runner:
         for k, (ins, count, s, d) in enumerate(burst):
             self.check(same_bits(host(d, np.float32), M.allreduce(ins, "FLOAT", "SUM")[r]), ("ll-burst", k, count))
         if os.environ.get("MPIGX_ZC_MIN"):
-            # LL launches (IN_PLACE Scan keeps LL under the forced zero-copy
-            # threshold) back to back with push two-shots, whose remote stores
-            # into the peers' arenas come before any barrier: the host inserts
-            # one after an LL launch (mpigx.cpp allreduce_push)
+            # LL launches (12 KB IN_PLACE Scans, below a 16 KiB zero-copy
+            # threshold) back to back with push two-shots (20 KB Allreduces,
+            # above it), whose remote stores into the peers' arenas come before
+            # any barrier: the host inserts one after an LL launch (mpigx.cpp
+            # allreduce_push)
+            zc_min = MPI.get_knob(self.comm, "ZC_MIN")
+            self.knob("ZC_MIN", 16384)
             self.knob("ALGO", "push")
             pairs = []
             for k in range(12):
@@ -347,6 +350,7 @@ class Runner:
             assert L.mpigx_comm_synchronize(cv) == 0
             L.mpigx_comm_set_blocking(cv, 1)
             self.knob("ALGO", None)
+            self.knob("ZC_MIN", zc_min)
             for k, (a, b, sa, sb, db) in enumerate(pairs):
                 self.check(same_bits(host(sa, np.int32), M.scan(a, "INT32_T", "SUM")[r]), ("ll-push-scan", k))
                 self.check(same_bits(host(db, np.float32), M.allreduce(b, "FLOAT", "SUM")[r]), ("ll-push-ar", k))
@@ -416,6 +420,27 @@ class Runner:
                 self.check(same_bits(host(rraw, np.float32)[1:], M.reduce(ins, "FLOAT", "SUM", root)),
                            ("unaligned reduce", algo))
         self.knob("ALGO", None)
+        # Scan / Exscan (zero-copy pull-push at n <= 8: element path when a
+        # buffer is off a 16-B boundary, vector path otherwise), in place too
+        ins = make("INT32_T", "MAX", n, count, 4701, edge=True)
+        hi = M.DTYPES["INT32_T"][0]
+        for coll, fn, ref in (("scan", L.mpigx_scan, M.scan(ins, "INT32_T", "MAX")),
+                              ("exscan", L.mpigx_exscan, M.exscan(ins, "INT32_T", "MAX"))):
+            for off, inplace in ((4, False), (4, True), (0, True)):
+                sraw = dev(np.concatenate([np.full(1, -7, np.int32), ins[r]]))
+                rraw = dev(np.full(count + 1, -7, np.int32)) if not inplace else sraw
+                s = ctypes.c_void_p(sraw.data_ptr() + off)
+                d = ctypes.c_void_p(rraw.data_ptr() + off)
+                if off == 0:  # aligned: the sentinel word goes to the end
+                    sraw = dev(np.concatenate([ins[r], np.full(1, -7, np.int32)]))
+                    rraw = sraw
+                    s = d = P(sraw)
+                rc = fn(IN_PLACE if inplace else s, d, count, hi, M.OPS["MAX"], cv)
+                self.check(rc == 0, ("unaligned", coll, off, inplace, "rc", rc))
+                got = host(rraw, np.int32)
+                body, sent = (got[1:], got[0]) if off else (got[:-1], got[-1])
+                exp = ref[r] if not (coll == "exscan" and r == 0) else (ins[0] if inplace else np.full(count, -7, np.int32))
+                self.check(same_bits(body, exp) and sent == -7, ("unaligned", coll, off, inplace))
 
     def ring_cases(self, nchs=(1, 2, 4)):
         """MPIGX_ALGO=ring (zero-copy path): bit-exact against the ring's own
