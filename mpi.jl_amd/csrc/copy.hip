@@ -133,6 +133,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
       for (int p = 0; p < n; ++p)
         if (p != r) ll_put(A.ll_push[p], 0, 0, flag);  // token: "I am in this launch"
     }
+    flush_remote_stores();
     if (!bc) {  // my own block (skipped in place)
       const char* own = a2a ? send + (long long)r * A.total : send;
       char* dst = recv + (long long)r * A.total;

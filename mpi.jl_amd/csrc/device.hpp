@@ -868,6 +868,30 @@ __device__ __forceinline__ void pull_release(int on) {
 // ---------------------------------------------------------------------------
 constexpr int kSigShift = 25;
 
+// Write-back of this XCD's L2 after stores into a PEER's signal array or LL
+// area, before the writer spins.  Those arrays are uncached in their owner's
+// mapping, but the owner's allocation flags do not carry over to an IPC import
+// (the peer's mapping is ordinary device memory), so a flag store can stay a
+// dirty line in the writer's L2 for as long as nothing writes that L2 back —
+// and a spinning writer issues no more fences.  Seen on the 1-GPU box (ranks
+// sharing the device): one rank saw none of its peers' entry words for 20 s
+// while every peer had passed the same barrier on its words
+// (tools/scan_repro.py, per-block phase stamps).  On distinct GPUs the line
+// would wait in the writer GPU's L2 the same way.  A LL sender's kernel
+// usually ended (end-of-kernel write-back) soon after its stores, which hid it
+// there; the LL two-shot polls between its two pushes.
+__device__ __forceinline__ void flush_remote_stores() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); }
+
+// One pause of a poll loop on a flag / LL line: s_sleep, and every 16th
+// pause a system-scope acquire (L1 + non-coherent L2 invalidate) so that a
+// copy of the polled line cached on this XCD cannot hide a peer's store for
+// longer than ~16 pauses (the stuck rank above polled words its peers had
+// written; this bounds the wait whichever side held the stale copy).
+__device__ __forceinline__ void spin_pause(unsigned& k) {
+  __builtin_amdgcn_s_sleep(1);
+  if ((++k & 15) == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
 // Phase timestamp k of this block (mpigx_comm_set_stamps, diagnostic): one
 // lane stores the 100 MHz device wall clock; a scalar branch when off.
 __device__ __forceinline__ void stamp(const PeerView& pv, int k) {
@@ -889,13 +913,19 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
       const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24) | (uint64_t)(key & 0xffffffu);
       uint64_t* peer_slot = pv.sig[lane] + (size_t)blockIdx.x * kMaxRanks + pv.rank;
       __hip_atomic_store(peer_slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      flush_remote_stores();
       uint64_t* mine = pv.sig[pv.rank] + (size_t)blockIdx.x * kMaxRanks + lane;
       const uint64_t t0 = wall_clock64();
       uint64_t v;
+      unsigned k = 0;
       while (((v = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> kSigShift) < ep) {
-        __builtin_amdgcn_s_sleep(1);
+        spin_pause(k);
         if (wall_clock64() - t0 > pv.timeout_ticks) {
           ok = false;
+          if (pv.stamps) {  // diagnostic: the epoch awaited and the word last seen from that peer
+            pv.stamps[(size_t)blockIdx.x * 8 + 6] = ep;
+            pv.stamps[(size_t)blockIdx.x * 8 + 7] = (v >> kSigShift) | ((uint64_t)lane << 56);
+          }
           break;
         }
       }
@@ -956,12 +986,14 @@ __device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t e
       if (s_last) {
         const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24);
         __hip_atomic_store(pv.sig[lane] + row + pv.rank, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        flush_remote_stores();
       }
       const uint64_t* mine = pv.sig[pv.rank] + row + lane;
       const uint64_t t0 = wall_clock64();
       uint64_t v;
+      unsigned k = 0;
       while (((v = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> kSigShift) < ep) {
-        __builtin_amdgcn_s_sleep(2);
+        spin_pause(k);
         if (wall_clock64() - t0 > pv.timeout_ticks) {
           ok = false;
           break;
@@ -1014,6 +1046,7 @@ __device__ __forceinline__ void ll_put(char* area, long long i, uint64_t d, unsi
 __device__ __forceinline__ bool ll_get(const char* area, long long i, unsigned flag, uint64_t t0, uint64_t timeout,
                                        uint64_t* d) {
   const uint64_t* q = reinterpret_cast<const uint64_t*>(area + kLLLine * i);
+  unsigned k = 0;
   for (;;) {
     const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1022,7 +1055,7 @@ __device__ __forceinline__ bool ll_get(const char* area, long long i, unsigned f
       return true;
     }
     if (wall_clock64() - t0 > timeout) return false;
-    __builtin_amdgcn_s_sleep(1);
+    spin_pause(k);
   }
 }
 // bytes [8i, 8i+8) ∩ [0, bytes) of dst <- d
@@ -1076,6 +1109,7 @@ __device__ __noinline__ bool ll_exchange(char* const* push, const char* in, long
     }
     *reinterpret_cast<uint64_t*>(unp + r * ustride + o) = d;
   }
+  flush_remote_stores();
   bool ok = true;
   const uint64_t t0 = wall_clock64();
   for (long long i = l0 + tid; i < l1 && ok; i += nt) {
@@ -1083,6 +1117,7 @@ __device__ __noinline__ bool ll_exchange(char* const* push, const char* in, long
       if (p == r) continue;
       const uint64_t* q = reinterpret_cast<const uint64_t*>(in + p * stride + kLLLine * i);
       uint64_t a, b;
+      unsigned k = 0;
       for (;;) {
         a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1091,7 +1126,7 @@ __device__ __noinline__ bool ll_exchange(char* const* push, const char* in, long
           ok = false;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        spin_pause(k);
       }
       if (ok) *reinterpret_cast<uint64_t*>(unp + p * ustride + 8 * i) = (a & 0xffffffffull) | (b << 32);
     }

@@ -378,6 +378,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       span(p, &c0, &cb, &l0, &l1);
       for (long long i = l0 + tid; i < l1; i += nt) ll_put(A.zc_recv[p], i, ll_pack8(send + c0 * es, i, cb), flag);
     }
+    flush_remote_stores();
     long long r0, rb, rl0, rl1;
     span(r, &r0, &rb, &rl0, &rl1);
     const long long rlo = r0 + lo, rhi = r0 + hi;
@@ -410,6 +411,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       for (int p = 0; p < n; ++p)
         if (p != r) ll_put(A.zc_recv[p] + half, i, d, flag);
     }
+    flush_remote_stores();
     for (int p = 0; p < n && ok; ++p) {
       if (p == r) continue;
       span(p, &c0, &cb, &l0, &l1);
@@ -661,6 +663,7 @@ __device__ __forceinline__ void ring_signal(const PeerView& pv, int to, uint64_t
     const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab ? 1 : 0) << 24);
     __hip_atomic_store(pv.sig[to] + (size_t)blockIdx.x * kMaxRanks + pv.rank, word, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+    flush_remote_stores();
   }
 }
 __device__ __forceinline__ bool ring_wait(const PeerView& pv, int from, uint64_t ep) {
@@ -669,8 +672,9 @@ __device__ __forceinline__ bool ring_wait(const PeerView& pv, int from, uint64_t
     const uint64_t* slot = pv.sig[pv.rank] + (size_t)blockIdx.x * kMaxRanks + from;
     const uint64_t t0 = wall_clock64();
     int ok = 1;
+    unsigned k = 0;
     while ((__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> kSigShift) < ep) {
-      __builtin_amdgcn_s_sleep(1);
+      spin_pause(k);
       if (wall_clock64() - t0 > pv.timeout_ticks) {
         ok = 0;
         __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

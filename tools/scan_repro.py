@@ -96,6 +96,9 @@ def main():
                     phase = {k: int((t[:, k] > 0).sum()) for k in range(6)}
                     t0 = int(t[started, 0].min()) if blocks else 0
                     first_missing = [int(b) for b in ((t[:, 1] == 0) & started).nonzero().flatten()[:8]]
+                    tmo = [(int(b), int(t[b, 6]), int(t[b, 7]) & ((1 << 56) - 1), int(t[b, 7]) >> 56)
+                           for b in (t[:, 6] != 0).nonzero().flatten()[:6]]
+                    print(json.dumps({"rank": r, "timeouts_block_ep_seen_lane": tmo}), flush=True)
                     print(json.dumps({"rank": r, "stamps_blocks": blocks, "stamps_phase_counts": phase,
                                       "entry_span_us": (int(t[started, 0].max()) - t0) / 100.0 if blocks else None,
                                       "blocks_stuck_at_entry": first_missing}), flush=True)

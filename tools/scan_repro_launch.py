@@ -1,24 +1,51 @@
 #!/usr/bin/env python3
-"""Start tools/scan_repro.py as N ranks on one GPU (tests/spmd_launch.py) and
-print every rank's JSON line.   python3 tools/scan_repro_launch.py 8"""
+"""Start tools/scan_repro.py as N ranks on one GPU and print every rank's
+result.  Each rank's output streams to gpurun_out/scan_repro_r<k>.log while
+it runs (progress is visible; nothing waits on a pipe).
+
+    python3 tools/scan_repro_launch.py 8 [path/to/libmpigx.so]"""
 import os
+import socket
+import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "tests"))
-
-from spmd_launch import launch  # noqa: E402
-
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-env = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS": "20000"}
+env0 = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS": "20000"}
 if len(sys.argv) > 2:
-    env["MPIGX_LIB"] = os.path.abspath(sys.argv[2])  # another build of libmpigx.so (A/B)
-rcs, outs = launch(os.path.join(ROOT, "tools", "scan_repro.py"), n, timeout=500, extra_env=env)
-for r, (rc, o) in enumerate(zip(rcs, outs)):
+    env0["MPIGX_LIB"] = os.path.abspath(sys.argv[2])  # another build of libmpigx.so (A/B)
+s = socket.socket()
+s.bind(("127.0.0.1", 0))
+port = s.getsockname()[1]
+s.close()
+out_dir = os.path.join(ROOT, "gpurun_out")
+os.makedirs(out_dir, exist_ok=True)
+procs, files = [], []
+for r in range(n):
+    env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), OMP_NUM_THREADS="1", **env0)
+    f = open(os.path.join(out_dir, f"scan_repro_r{r}.log"), "w")
+    files.append(f)
+    procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tools", "scan_repro.py")], env=env,
+                                  cwd=ROOT, stdout=f, stderr=subprocess.STDOUT, start_new_session=True))
+t0 = time.time()
+while any(p.poll() is None for p in procs) and time.time() - t0 < 280:
+    time.sleep(5)
+    print(f"[{time.time() - t0:.0f}s] running: {[r for r, p in enumerate(procs) if p.poll() is None]}", flush=True)
+for p in procs:
+    if p.poll() is None:
+        os.killpg(p.pid, 9)
+        p.wait()
+for f in files:
+    f.close()
+for r, p in enumerate(procs):
+    o = open(os.path.join(out_dir, f"scan_repro_r{r}.log")).read()
     lines = [l for l in o.splitlines() if l.startswith("{")]
     prog = [l for l in o.splitlines() if l.startswith(f"r{r} ")]
-    print(f"rank {r} rc={rc} last={prog[-1] if prog else None}", *(lines[-2:] if lines else [o[-1500:]]), flush=True)
-    if rc and os.environ.get("MPIGX_DIAG_TRACE"):
+    print(f"rank {r} rc={p.returncode} last={prog[-1] if prog else None}", *(lines[-2:] if lines else [o[-800:]]),
+          flush=True)
+    if p.returncode and os.environ.get("MPIGX_DIAG_TRACE"):
         ev = [l for l in o.splitlines() if l.startswith("[trace") or l.startswith(f"r{r} ")]
         print("\n".join(ev[-14:]), flush=True)
-sys.exit(0 if all(rc == 0 for rc in rcs) else 1)
+sys.exit(0 if all(p.returncode == 0 for p in procs) else 1)
