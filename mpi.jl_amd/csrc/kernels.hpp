@@ -36,9 +36,14 @@ __device__ __forceinline__ void signal_done(const PeerView& pv, int aborted = 0)
     if (threadIdx.x == 0) {
       const unsigned long long prev =
           __hip_atomic_fetch_add(pv.dcount, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == pv.dbase + gridDim.x - 1)
+      if (prev == pv.dbase + gridDim.x - 1) {
         __hip_atomic_store(pv.done, (pv.seq << 1) | (aborted ? 1ull : 0ull), __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+        // push the word out now, not at some later system-scope release
+        // (device.hpp flush_remote_stores): a host spinning on it saw it only
+        // after its own hipStreamSynchronize fallback, 20 s late (r03r)
+        flush_remote_stores();
+      }
     }
   }
 }

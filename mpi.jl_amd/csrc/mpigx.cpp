@@ -322,11 +322,19 @@ int finish(mpigx_comm* c) {
       // keep point-to-point rendezvous moving while blocked here (a peer may
       // wait on our acknowledgement before it joins this collective)
       if ((spins & 63) == 0) rt::progress_all(c);
-      if ((++spins & 1023) == 0 && now_s() - t0 > limit) {
-        HIPCK(hipStreamSynchronize(c->stream));
-        w = *c->done;
-        c->done_target = w >> 1;
-        break;
+      if ((++spins & 1023) == 0) {
+        const double el = now_s() - t0;
+        // the stream already drained but the word has not shown up: take the
+        // stream's own completion (its end-of-kernel release) after 20 ms
+        // instead of the full limit (r03r: ranks 1 and 3 of 8 sharing the
+        // GPU left a completed Scan 20 s after their peers this way)
+        if (el > limit || (el > 0.02 && hipStreamQuery(c->stream) == hipSuccess)) {
+          HIPCK(hipStreamSynchronize(c->stream));
+          for (int i = 0; i < 100000 && ((w = *c->done) >> 1) < c->done_target; ++i) {
+          }
+          c->done_target = w >> 1;
+          break;
+        }
       }
     }
     // the last launch's zero-copy verdict (kernels.hpp signal_done)
