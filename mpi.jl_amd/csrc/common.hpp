@@ -12,6 +12,15 @@ namespace mpigx {
 
 constexpr int kMaxRanks = MPIGX_MAX_RANKS;
 constexpr int kMaxBlocks = 1024;      // signal slots per rank per barrier
+// One 128-B cache line per signal slot [block][rank]: a peer writes its slot
+// through its IPC import of my array, which is not uncached there, and a
+// line shared by several writers came back with one writer's stale copy of
+// another's word (8 ranks on one GPU: rank 0 saw the root's previous epoch
+// forever while every other rank saw its new one).
+constexpr int kSigStride = 16;        // u64 words per slot
+__host__ __device__ constexpr size_t sig_index(size_t block, int rank) {
+  return (block * kMaxRanks + (size_t)rank) * kSigStride;
+}
 constexpr int kThreads = 256;         // threads per block of every kernel
 
 // Element representations.  Several MPI handles share one (INT == INT32_T,

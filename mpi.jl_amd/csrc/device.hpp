@@ -911,10 +911,10 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
     bool ok = true, ab = false;
     if (lane < pv.n) {
       const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24) | (uint64_t)(key & 0xffffffu);
-      uint64_t* peer_slot = pv.sig[lane] + (size_t)blockIdx.x * kMaxRanks + pv.rank;
+      uint64_t* peer_slot = pv.sig[lane] + sig_index(blockIdx.x, pv.rank);
       __hip_atomic_store(peer_slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       flush_remote_stores();
-      uint64_t* mine = pv.sig[pv.rank] + (size_t)blockIdx.x * kMaxRanks + lane;
+      uint64_t* mine = pv.sig[pv.rank] + sig_index(blockIdx.x, lane);
       const uint64_t t0 = wall_clock64();
       uint64_t v;
       unsigned k = 0;
@@ -979,16 +979,16 @@ __device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t e
   __syncthreads();
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    const size_t row = (size_t)kMaxBlocks * kMaxRanks;
+    const size_t row = kMaxBlocks;  // the whole-launch row after the per-block ones
     if (s_last) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     bool ok = true, ab = false;
     if (lane < pv.n) {
       if (s_last) {
         const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24);
-        __hip_atomic_store(pv.sig[lane] + row + pv.rank, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(pv.sig[lane] + sig_index(row, pv.rank), word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         flush_remote_stores();
       }
-      const uint64_t* mine = pv.sig[pv.rank] + row + lane;
+      const uint64_t* mine = pv.sig[pv.rank] + sig_index(row, lane);
       const uint64_t t0 = wall_clock64();
       uint64_t v;
       unsigned k = 0;

@@ -666,7 +666,7 @@ __device__ __forceinline__ void ring_signal(const PeerView& pv, int to, uint64_t
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab ? 1 : 0) << 24);
-    __hip_atomic_store(pv.sig[to] + (size_t)blockIdx.x * kMaxRanks + pv.rank, word, __ATOMIC_RELAXED,
+    __hip_atomic_store(pv.sig[to] + sig_index(blockIdx.x, pv.rank), word, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     flush_remote_stores();
   }
@@ -674,7 +674,7 @@ __device__ __forceinline__ void ring_signal(const PeerView& pv, int to, uint64_t
 __device__ __forceinline__ bool ring_wait(const PeerView& pv, int from, uint64_t ep) {
   __shared__ int s_ok;
   if (threadIdx.x == 0) {
-    const uint64_t* slot = pv.sig[pv.rank] + (size_t)blockIdx.x * kMaxRanks + from;
+    const uint64_t* slot = pv.sig[pv.rank] + sig_index(blockIdx.x, from);
     const uint64_t t0 = wall_clock64();
     int ok = 1;
     unsigned k = 0;

@@ -1817,7 +1817,7 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   HIPCK(hipMalloc(&c->stage, c->stage_bytes));
   // rows [0, kMaxBlocks): per-block barriers; row kMaxBlocks: whole-launch
   // barrier (device.hpp rank_barrier_grid)
-  const size_t sig_bytes = (size_t)(kMaxBlocks + 1) * kMaxRanks * sizeof(uint64_t);
+  const size_t sig_bytes = sig_index(kMaxBlocks + 1, 0) * sizeof(uint64_t);
   HIPCK(hipExtMallocWithFlags((void**)&c->sig, sig_bytes, hipDeviceMallocUncached));
   HIPCK(hipMemset(c->sig, 0, sig_bytes));
   // LL area for small messages (M_AR_LL ...): uncached like the signal array,
