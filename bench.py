@@ -372,8 +372,10 @@ def bench_allreduce(args):
     errors, alive = {}, [True]
     section_s = {"headline": round(time.perf_counter() - t_start, 2)}  # wall seconds per section (rank 0)
 
-    def guarded(name, fn, default=None):
-        if not alive[0]:
+    def guarded(name, fn, default=None, engine=True):
+        # engine=False: the section does not call libmpigx (RCCL), so it runs
+        # even after an engine section broke the communicator
+        if engine and not alive[0]:
             errors[name] = "skipped after an earlier failure"
             return default
         t_sec = time.perf_counter()
@@ -384,10 +386,10 @@ def bench_allreduce(args):
             errors[name] = f"{type(e).__name__}: {str(e)[:200]}"
         (anybad,) = tmax(bad)
         section_s[name] = round(time.perf_counter() - t_sec, 2)
-        if not anybad:  # back to the defaults (collective: every rank is here)
+        if engine and not anybad and alive[0]:  # back to the defaults (collective: every rank is here)
             MPI.set_knob(comm, "ALGO", None)
             MPI.set_knob(comm, "RING_CHANNELS", 1)
-        if anybad:
+        if anybad and engine:
             alive[0] = False
         return out
 
@@ -421,54 +423,6 @@ def bench_allreduce(args):
                 "read_over_algorithmic": round(rd / algo_x, 4), "source": "amd-smi gpu_metrics xgmi_*_data_acc",
                 "steps": reps}
     xg = guarded("xgmi_counters", xgmi_section)
-
-    # measured xGMI: every rank pulls 64 MiB from every peer at once / from one peer
-    def probe_section():
-        probe = {}
-        for kind, name in ((0, "all_peers"), (1, "one_link")):
-            secs = ctypes.c_double(0)
-            pb = 64 << 20
-            for _ in range(2):  # warm, then timed
-                rc = MPI.lib().mpigx_comm_probe(comm.val, kind, pb, ctypes.byref(secs))
-                if rc:
-                    raise RuntimeError(f"mpigx_comm_probe returned {rc}")
-            (sec,) = tmax(secs.value)
-            probe[name + "_GBps"] = round(pb * ((n - 1) if kind == 0 else 1) / sec / 1e9, 1)
-        return probe
-    probe = guarded("xgmi_probe", probe_section, {})
-
-    # where the headline call's time goes: per-block phase timestamps of the
-    # kernel (mpigx_comm_set_stamps, 100 MHz device clock) on one more call of
-    # each two-shot variant at the headline size; median over blocks of each
-    # phase, and the span from the first block's entry to the last block's exit
-    def phases_section():
-        out = {}
-        st = torch.zeros(1024 * 8, dtype=torch.int64, device=dev)
-        xs = rank_input(rank, S // 4)
-        xr = torch.empty_like(xs)
-        names = ("entry_barrier", "reduce_scatter", "mid_barrier", "allgather", "exit_barrier")
-        for algo in ("pull", "pull_generic", "push", "pullpush"):
-            MPI.set_knob(comm, "ALGO", algo)
-            for _ in range(2):
-                MPI.Allreduce_(xs, xr, MPI.SUM, comm)
-            st.zero_()
-            MPI.lib().mpigx_comm_set_stamps(comm.val, ctypes.c_void_p(st.data_ptr()))
-            MPI.Allreduce_(xs, xr, MPI.SUM, comm)
-            torch.cuda.synchronize()
-            MPI.lib().mpigx_comm_set_stamps(comm.val, None)
-            t = st.view(1024, 8)[:, :6].cpu().numpy().astype(np.int64)
-            t = t[t[:, 0] > 0]
-            d = np.diff(t, axis=1) / 100.0  # us
-            rec = {nm: round(float(np.median(d[:, k])), 2) for k, nm in enumerate(names)}
-            rec["blocks"] = int(t.shape[0])
-            rec["span_us"] = round(float(t[:, 5].max() - t[:, 0].min()) / 100.0, 2)
-            rec["reduce_scatter_max_us"] = round(float(d[:, 1].max()), 2)
-            rec["allgather_max_us"] = round(float(d[:, 3].max()), 2)
-            out[algo] = rec
-        MPI.set_knob(comm, "ALGO", None)
-        del xs, xr, st
-        return out
-    phases = guarded("phases", phases_section, {})
 
     # size sweep (mpigx), algorithm variants, the ring (MPIGX_ALGO=ring, one
     # ring / every coprime-stride ring) and the RCCL comparison point
@@ -541,7 +495,55 @@ def bench_allreduce(args):
                     rccl[f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"] = round(busbw(nb, tw), 1)
             except Exception as e:  # noqa: BLE001
                 rccl["error"] = str(e)[:200]
-    guarded("rccl", rccl_section)
+    guarded("rccl", rccl_section, engine=False)
+
+    # measured xGMI: every rank pulls 64 MiB from every peer at once / from one peer
+    def probe_section():
+        probe = {}
+        for kind, name in ((0, "all_peers"), (1, "one_link")):
+            secs = ctypes.c_double(0)
+            pb = 64 << 20
+            for _ in range(2):  # warm, then timed
+                rc = MPI.lib().mpigx_comm_probe(comm.val, kind, pb, ctypes.byref(secs))
+                if rc:
+                    raise RuntimeError(f"mpigx_comm_probe returned {rc}")
+            (sec,) = tmax(secs.value)
+            probe[name + "_GBps"] = round(pb * ((n - 1) if kind == 0 else 1) / sec / 1e9, 1)
+        return probe
+    probe = guarded("xgmi_probe", probe_section, {})
+
+    # where the headline call's time goes: per-block phase timestamps of the
+    # kernel (mpigx_comm_set_stamps, 100 MHz device clock) on one more call of
+    # each two-shot variant at the headline size; median over blocks of each
+    # phase, and the span from the first block's entry to the last block's exit
+    def phases_section():
+        out = {}
+        st = torch.zeros(1024 * 8, dtype=torch.int64, device=dev)
+        xs = rank_input(rank, S // 4)
+        xr = torch.empty_like(xs)
+        names = ("entry_barrier", "reduce_scatter", "mid_barrier", "allgather", "exit_barrier")
+        for algo in ("pull", "pull_generic", "push", "pullpush"):
+            MPI.set_knob(comm, "ALGO", algo)
+            for _ in range(2):
+                MPI.Allreduce_(xs, xr, MPI.SUM, comm)
+            st.zero_()
+            MPI.lib().mpigx_comm_set_stamps(comm.val, ctypes.c_void_p(st.data_ptr()))
+            MPI.Allreduce_(xs, xr, MPI.SUM, comm)
+            torch.cuda.synchronize()
+            MPI.lib().mpigx_comm_set_stamps(comm.val, None)
+            t = st.view(1024, 8)[:, :6].cpu().numpy().astype(np.int64)
+            t = t[t[:, 0] > 0]
+            d = np.diff(t, axis=1) / 100.0  # us
+            rec = {nm: round(float(np.median(d[:, k])), 2) for k, nm in enumerate(names)}
+            rec["blocks"] = int(t.shape[0])
+            rec["span_us"] = round(float(t[:, 5].max() - t[:, 0].min()) / 100.0, 2)
+            rec["reduce_scatter_max_us"] = round(float(d[:, 1].max()), 2)
+            rec["allgather_max_us"] = round(float(d[:, 3].max()), 2)
+            out[algo] = rec
+        MPI.set_knob(comm, "ALGO", None)
+        del xs, xr, st
+        return out
+    phases = guarded("phases", phases_section, {})
 
     def time_call(call, steps, warmup, prelude=0):
         for _ in range(prelude + warmup):  # prelude: the tuners' sampling calls
@@ -604,6 +606,15 @@ def bench_allreduce(args):
     # bit-exact against the fold of every rank's (regenerated) input
     cfg5, cfg5_ok = {}, [True]
     def config5_section():
+        # its own, shorter device timeout: a stall here fails this section in
+        # 20 s instead of the default 60 s (every earlier number is printed anyway)
+        MPI.lib().mpigx_comm_set_timeout(comm.val, 20000)
+        try:
+            config5_body()
+        finally:
+            MPI.lib().mpigx_comm_set_timeout(comm.val, int(os.environ.get("MPIGX_TIMEOUT_MS", 60000)))
+
+    def config5_body():
         if not args.no_extra:
             ops = (("BAND", MPI.BAND, torch.bitwise_and), ("BOR", MPI.BOR, torch.bitwise_or),
                    ("MAX", MPI.MAX, torch.maximum))

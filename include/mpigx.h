@@ -121,6 +121,13 @@ int mpigx_get_unique_id(mpigx_unique_id_t *id);
 int mpigx_comm_init_rank(mpigx_comm_t *comm, int nranks, const mpigx_unique_id_t *id,
                          int rank, int device);
 int mpigx_comm_free(mpigx_comm_t comm);
+/* Local release (no barrier; MPI.jl's GC finalizers, comm.jl:82): waits for
+ * this rank's queued work on `comm`, then unmaps the peers' memory and frees
+ * its own.  Valid once this rank's last call on `comm` has returned — every
+ * collective's final barrier retires the peers' accesses to this rank's
+ * memory — so ranks may release at different times.  mpigx_comm_free is the
+ * collective form (a barrier first). */
+int mpigx_comm_release(mpigx_comm_t comm);
 /* MPI_Comm_split — comm.jl:92-105.  Collective; color = MPIGX_UNDEFINED
  * (-32766) gives *newcomm = NULL.  Members keep the parent's device. */
 int mpigx_comm_split(mpigx_comm_t comm, int color, int key, mpigx_comm_t *newcomm);
@@ -199,6 +206,10 @@ int mpigx_comm_device_share(mpigx_comm_t comm, int *ranks, int *cap);
  * reduce-scatter, 3 after the middle barrier, 4 after the allgather, 5 after
  * the exit barrier.  Local (not collective). */
 int mpigx_comm_set_stamps(mpigx_comm_t comm, void *stamps);
+/* How long a collective's blocks wait for a peer before the call fails with
+ * MPI_ERR_OTHER and the communicator is marked broken (default
+ * MPIGX_TIMEOUT_MS, 60000).  Local; applies to later calls.  ms >= 1. */
+int mpigx_comm_set_timeout(mpigx_comm_t comm, long long ms);
 /* Zero-copy paths (user buffers mapped by the peers over IPC): how many
  * launches ran on a cached view without any host exchange, and how many
  * host exchanges of buffer registrations there were.  Diagnostic. */

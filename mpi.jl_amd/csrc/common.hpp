@@ -97,6 +97,11 @@ enum FoldMode : int {
 // no fence and no separate signal.  A rank's LL area (uncached HBM,
 // IPC-mapped by every peer) is [2 parities][kMaxRanks senders][ll_stride].
 constexpr int kLLLine = 16;
+// Payload bytes per block slice of an LL exchange are a multiple of this: 64
+// payload bytes = 8 LL lines = one 128-B cache line of the receiver's area, so
+// no two blocks of a sender (possibly on two XCDs, each with its own L2 copy
+// of the line) write parts of one cache line.
+constexpr int kLLAlign = 64;
 
 // Copy-kernel modes (Bcast / Allgather / Alltoall / Barrier).
 //   C_BCAST     : every non-root pulls the whole buffer from the root (small)
@@ -144,6 +149,8 @@ struct PeerView {
   // this launch
   unsigned long long wbase;
   unsigned long long fbase;
+  int sig_mode;                // signal store / poll variant (device.hpp sig_put / sig_get)
+  int pad_;
 };
 
 // Fold-kernel arguments.  Sources/partition are resolved on the host.

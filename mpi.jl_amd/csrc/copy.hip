@@ -23,6 +23,7 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(CopyArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
+  stamp(sA.pv, 0);
   const int ab = copy_body<NMAX, U>(sA);
   signal_done(sA.pv, ab);
 }

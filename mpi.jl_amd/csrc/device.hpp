@@ -867,6 +867,11 @@ __device__ __forceinline__ void pull_release(int on) {
 // Returns false (and sets *err) if a peer did not arrive within the timeout.
 // ---------------------------------------------------------------------------
 constexpr int kSigShift = 25;
+// Error word values (PeerView.err; host: mpigx.cpp finish): a peer did not
+// arrive in time (MPI_ERR_OTHER), or the protocol itself was violated — a
+// signal word beyond what any peer can have stored yet, a kernel
+// precondition that does not hold (MPI_ERR_INTERN).
+constexpr unsigned kErrTimeout = 1u, kErrProtocol = 2u;
 
 // Write-back of this XCD's L2 after stores into a PEER's signal array or LL
 // area, before the writer spins.  Those arrays are uncached in their owner's
@@ -898,6 +903,26 @@ __device__ __forceinline__ void stamp(const PeerView& pv, int k) {
   if (pv.stamps && threadIdx.x == 0) pv.stamps[(size_t)blockIdx.x * 8 + k] = wall_clock64();
 }
 
+// A zero the compiler cannot see through (an `atomicrmw or 0` is folded into
+// a plain load otherwise).
+__device__ __forceinline__ uint64_t opaque_zero() {
+  uint64_t z = 0;
+  asm volatile("" : "+v"(z));
+  return z;
+}
+// Signal word into a peer's slot (sig_mode bit 0: atomic swap instead of a
+// store), and a poll of my own slot (bit 2: read-modify-write read).
+__device__ __forceinline__ void sig_put(uint64_t* slot, uint64_t word, int mode) {
+  if (mode & 1) (void)__hip_atomic_exchange(slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else __hip_atomic_store(slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  flush_remote_stores();
+}
+__device__ __forceinline__ uint64_t sig_get(const uint64_t* slot, int mode) {
+  if (mode & 4) return __hip_atomic_fetch_add(const_cast<uint64_t*>(slot), opaque_zero(), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, int* abort = nullptr,
                                              unsigned key = 0, bool check_key = false, bool fences = true) {
   __shared__ int s_fail, s_abort;
@@ -908,36 +933,54 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
     const int lane = threadIdx.x;
     if (fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bool ok = true, ab = false;
+    bool ok = true, ab = false, bad = false;
     if (lane < pv.n) {
+      const int mode = pv.sig_mode;
       const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24) | (uint64_t)(key & 0xffffffu);
       uint64_t* peer_slot = pv.sig[lane] + sig_index(blockIdx.x, pv.rank);
-      __hip_atomic_store(peer_slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      flush_remote_stores();
+      sig_put(peer_slot, word, mode);
       uint64_t* mine = pv.sig[pv.rank] + sig_index(blockIdx.x, lane);
       const uint64_t t0 = wall_clock64();
       uint64_t v;
       unsigned k = 0;
-      while (((v = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> kSigShift) < ep) {
+      while (((v = sig_get(mine, mode)) >> kSigShift) < ep) {
         spin_pause(k);
+        if ((mode & 2) && (k & 63) == 0) sig_put(peer_slot, word, mode);  // republish my word
         if (wall_clock64() - t0 > pv.timeout_ticks) {
           ok = false;
           if (pv.stamps) {  // diagnostic: the epoch awaited and the word last seen from that peer
             pv.stamps[(size_t)blockIdx.x * 8 + 6] = ep;
             pv.stamps[(size_t)blockIdx.x * 8 + 7] = (v >> kSigShift) | ((uint64_t)lane << 56);
+            pv.stamps[(size_t)blockIdx.x * 8 + 2] = wall_clock64();  // when this block gave up
+            // the same slot read three other ways: RMW, non-temporal, after an acquire
+            pv.stamps[(size_t)blockIdx.x * 8 + 3] =
+                __hip_atomic_fetch_add(mine, opaque_zero(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> kSigShift;
+            pv.stamps[(size_t)blockIdx.x * 8 + 4] = __builtin_nontemporal_load(mine) >> kSigShift;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            pv.stamps[(size_t)blockIdx.x * 8 + 5] =
+                __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> kSigShift;
           }
           break;
         }
+      }
+      // A peer can be at most one barrier ahead of me (it cannot pass this
+      // one before my word for it arrived): a word beyond ep + 1 means the
+      // ranks' epochs diverged — fail loudly instead of passing on it.
+      if (ok && (v >> kSigShift) > ep + 1) {
+        ok = false;
+        bad = true;
       }
       ab = ok && (((v >> 24) & 1u) || (check_key && (v >> kSigShift) == ep && (v & 0xffffffu) != (key & 0xffffffu)));
     }
     const bool all_ok = __all(ok);
     const bool any_ab = __any(ab);
+    const bool any_bad = __any(bad);
     if (fences) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (lane == 0) {
       s_fail = all_ok ? 0 : 1;
       s_abort = (ab_in || any_ab) ? 1 : 0;
-      if (!all_ok) __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (!all_ok)
+        __hip_atomic_store(pv.err, any_bad ? kErrProtocol : kErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   __syncthreads();

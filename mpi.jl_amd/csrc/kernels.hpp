@@ -80,6 +80,7 @@ __global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(FoldArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
+  stamp(sA.pv, 0);
   const int ab = fold_body<OP, T, NMAX, SCHED>(sA);
   signal_done(sA.pv, ab);
 }
@@ -215,8 +216,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
     }
     stamp(pv, 4);
-    rank_barrier_exit(pv, ep++, &ab);  // nobody reads my buffers any more
-    stamp(pv, 5);
+    if (rank_barrier_exit(pv, ep++, &ab)) stamp(pv, 5);  // nobody reads my buffers any more
     return ab;
   }
 
@@ -333,8 +333,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     block_gather_u<NMAX, FU>(dsts, srcs, lens, n - 1);
     }
     stamp(pv, 4);
-    rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
-    stamp(pv, 5);
+    if (rank_barrier(pv, ep++, &ab)) stamp(pv, 5);  // every slice of my recvbuf has arrived
     return ab;
   }
 
@@ -590,7 +589,7 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
       stamp(pv, 2);
       stamp(pv, 3);
       stamp(pv, 4);
-      rank_barrier_grid(pv, ep++, &ab);  // every rank's blocks are done: my recvbuf is complete
+      if (rank_barrier_grid(pv, ep++, &ab)) stamp(pv, 5);  // every rank's blocks are done: my recvbuf is complete
     } else {
       if (!ab) {
         const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
@@ -599,9 +598,8 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
       stamp(pv, 2);
       stamp(pv, 3);
       stamp(pv, 4);
-      rank_barrier(pv, ep++, &ab);  // every slice of my recvbuf has arrived
+      if (rank_barrier(pv, ep++, &ab)) stamp(pv, 5);  // every slice of my recvbuf has arrived
     }
-    stamp(pv, 5);
     signal_done(pv, ab);
     return;
   }
@@ -638,8 +636,7 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
     block_gather_u<MP, U>(dsts, srcs, lens, n - 1);
   }
   stamp(pv, 4);
-  rank_barrier_exit(pv, ep++, &ab);  // nobody reads my buffers any more
-  stamp(pv, 5);
+  if (rank_barrier_exit(pv, ep++, &ab)) stamp(pv, 5);  // nobody reads my buffers any more
   signal_done(pv, ab);
 }
 
@@ -962,9 +959,22 @@ __device__ __forceinline__ int scan_pp_body(const ScanArgs& A) {
   if (!ab) {
     const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
     const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
-    constexpr int U = vec_regs<T>() <= 4 ? 2 : 1;
-    if (A.exclusive) scan_pp_span<OP, T, true, U>(A, lo, hi);
-    else scan_pp_span<OP, T, false, U>(A, lo, hi);
+    // preconditions of every access below, checked instead of trusted: a
+    // violation stores nothing and fails the call (MPI_ERR_INTERN) instead of
+    // faulting the GPU (round 3 saw an aperture violation in this kernel)
+    bool sane = pv.n >= 2 && pv.n <= 8 && r < pv.n && 0 <= c0 && c0 <= lo && lo <= hi && hi <= c1 &&
+                c1 <= A.count;
+    for (int q = 0; q < pv.n; ++q) sane &= A.src[q] != nullptr && A.zrecv[q] != nullptr;
+    if (!sane) {
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(pv.err, kErrProtocol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (pv.stamps) pv.stamps[(size_t)b * 8 + 6] = 0xBAD0000000000000ull | (uint64_t)(hi - lo);
+      }
+    } else {
+      constexpr int U = vec_regs<T>() <= 4 ? 2 : 1;
+      if (A.exclusive) scan_pp_span<OP, T, true, U>(A, lo, hi);
+      else scan_pp_span<OP, T, false, U>(A, lo, hi);
+    }
   }
   rank_barrier(pv, ep++, &ab);  // publishes my stores into the peers' recvbufs
   return ab;
@@ -984,6 +994,7 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(ScanArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
+  stamp(sA.pv, 0);
   const int ab = sA.pp ? scan_pp_body<OP, T>(sA) : scan_body<OP, T>(sA);
   signal_done(sA.pv, ab);
 }

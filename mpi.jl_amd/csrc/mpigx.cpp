@@ -15,6 +15,7 @@
 //     into MPI error classes.
 #include <errno.h>
 #include <fcntl.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -270,6 +271,7 @@ PeerView make_view(mpigx_comm* c) {
   pv.fbase = c->wfinished;
   pv.seq = c->launch_seq + 1;
   pv.stamps = c->stamps;
+  pv.sig_mode = c->sig_mode;
   for (int p = 0; p < c->n; ++p) {
     pv.sig[p] = c->peer_sig[p];
     pv.stage[p] = c->peer_stage[p];
@@ -279,10 +281,9 @@ PeerView make_view(mpigx_comm* c) {
 
 // Account for one launch of `grid` blocks made with view `pv`.
 void note_launch(mpigx_comm* c, const PeerView& pv, unsigned grid) {
-  static const bool diag = getenv("MPIGX_DIAG_TRACE") != nullptr;  // DIAG (temporary)
-  if (diag)
-    fprintf(stderr, "[trace r%d] launch epoch=%llu grid=%u key=%u bad=%d dbase=%llu seq=%llu\n", c->rank,
-            (unsigned long long)pv.epoch, grid, pv.zc_key, pv.zc_bad, (unsigned long long)pv.dbase,
+  if (c->diag_trace)  // diagnostic launch trace (MPIGX_DIAG_TRACE, read at init)
+    fprintf(stderr, "[trace r%d] t=%.6f launch epoch=%llu grid=%u key=%u bad=%d dbase=%llu seq=%llu\n", c->rank,
+            now_s(), (unsigned long long)pv.epoch, grid, pv.zc_key, pv.zc_bad, (unsigned long long)pv.dbase,
             (unsigned long long)pv.seq);
   if (c->launch_pending) {
     c->last_prelaunch_s = now_s() - c->t_entry;
@@ -324,25 +325,34 @@ int finish(mpigx_comm* c) {
       if ((spins & 63) == 0) rt::progress_all(c);
       if ((++spins & 1023) == 0) {
         const double el = now_s() - t0;
-        // the stream already drained but the word has not shown up: take the
-        // stream's own completion (its end-of-kernel release) after 20 ms
-        // instead of the full limit (r03r: ranks 1 and 3 of 8 sharing the
-        // GPU left a completed Scan 20 s after their peers this way)
-        if (el > limit || (el > 0.02 && hipStreamQuery(c->stream) == hipSuccess)) {
+        // The completion word is the only source of the zero-copy verdict, so
+        // it is never replaced by an older one.  A stream that drained without
+        // it (every block of the last launch counts itself and the last one
+        // stores the word before the kernel ends) means the word is lost —
+        // a protocol failure, reported, not guessed past.
+        if (el > limit || (el > 0.05 && hipStreamQuery(c->stream) == hipSuccess)) {
           HIPCK(hipStreamSynchronize(c->stream));
-          for (int i = 0; i < 100000 && ((w = *c->done) >> 1) < c->done_target; ++i) {
+          const double t1 = now_s();
+          while (((w = *c->done) >> 1) < c->done_target && now_s() - t1 < 1.0) sched_yield();
+          if ((w >> 1) < c->done_target) {
+            fprintf(stderr, "[mpigx] rank %d: completion word %llu never arrived for launch %llu (stream drained)\n",
+                    c->rank, (unsigned long long)(w >> 1), (unsigned long long)c->done_target);
+            c->broken = true;
+            c->last_aborted = false;
+            return MPIGX_ERR_INTERN;
           }
-          c->done_target = w >> 1;
           break;
         }
       }
     }
-    // the last launch's zero-copy verdict (kernels.hpp signal_done)
-    c->last_aborted = (w & 1) != 0;
+    // the last launch's zero-copy verdict (kernels.hpp signal_done): only
+    // from the word of exactly that launch
+    c->last_aborted = (w >> 1) == c->done_target && (w & 1) != 0;
   }
-  if (__atomic_load_n(c->err, __ATOMIC_ACQUIRE) != 0) {
+  if (const unsigned e = __atomic_load_n(c->err, __ATOMIC_ACQUIRE)) {
+    // device.hpp kErrTimeout (a peer did not arrive) / kErrProtocol
     c->broken = true;
-    return MPIGX_ERR_OTHER;
+    return e == 2 ? MPIGX_ERR_INTERN : MPIGX_ERR_OTHER;
   }
   return MPIGX_SUCCESS;
 }
@@ -1038,6 +1048,10 @@ bool copy_ll_take(mpigx_comm* c, long long bytes) { return ll_fits(c, bytes); }
 // run.  Every rank sees the same calls and outcomes (blocking mode,
 // MPIGX_AR_TUNE and the zero-copy verdict agree), so the exchange in
 // ar_tune_note is collective.
+// the pull-push two-shot exists only as the dedicated kernel (n <= 8, MPICH
+// tree order); elsewhere allreduce_zc runs the pull for it, so it is not timed
+bool ar_pullpush_ok(const mpigx_comm* c) { return c->n >= 2 && c->n <= 8 && c->order != MPIGX_ORDER_LINEAR; }
+
 int ar_tune_pick(mpigx_comm* c, int* variant) {
   if (c->ar_choice >= 0) {
     *variant = c->ar_choice;
@@ -1047,7 +1061,8 @@ int ar_tune_pick(mpigx_comm* c, int* variant) {
   if (!c->ar_tune || !c->blocking || c->sync_mode != 1 || !c->ar_ev[0]) return -1;
   const int step = c->ar_step++;
   if (step == 0) return -1;  // registration call (host exchange, first imports)
-  *variant = (step - 1) % 3;  // pull, push, pull-push (again if a call fell back to staging)
+  // pull, push, pull-push (again if a call fell back to staging)
+  *variant = (step - 1) % (ar_pullpush_ok(c) ? 3 : 2);
   return *variant;
 }
 int ar_tune_note(mpigx_comm* c, int variant, long long bytes) {
@@ -1056,14 +1071,16 @@ int ar_tune_note(mpigx_comm* c, int variant, long long bytes) {
   HIPCK(hipEventSynchronize(c->ar_ev[1]));
   HIPCK(hipEventElapsedTime(&ms, c->ar_ev[0], c->ar_ev[1]));
   c->ar_spb[variant] = (ms / 1e3) / (double)bytes;
-  if (variant != 2 || c->ar_spb[0] <= 0 || c->ar_spb[1] <= 0) return MPIGX_SUCCESS;
+  const bool pp = ar_pullpush_ok(c);
+  if (variant != (pp ? 2 : 1) || c->ar_spb[0] <= 0 || c->ar_spb[1] <= 0) return MPIGX_SUCCESS;
+  if (!pp) c->ar_spb[2] = -1;  // not available: never chosen, reported as -1
   double mine[3] = {c->ar_spb[0], c->ar_spb[1], c->ar_spb[2]}, all[kMaxRanks][3];
   const int rc = host_allgather(c, mine, sizeof mine, all);
   if (rc) return rc;
   double w[3] = {0, 0, 0};
   for (int q = 0; q < c->n; ++q)
     for (int k = 0; k < 3; ++k) w[k] = all[q][k] > w[k] ? all[q][k] : w[k];
-  int best = w[1] < w[2] ? 1 : 2;
+  int best = (!pp || w[1] < w[2]) ? 1 : 2;
   c->ar_choice = w[best] < 0.97 * w[0] ? best : 0;
   return MPIGX_SUCCESS;
 }
@@ -1261,7 +1278,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
       ptrs[q] = q == c->rank ? send : (const void*)(c->stage + q * ustride - c0 * es);
     plan_schedule(c, a, n, 0, count, es, ptrs, &nmax, &sched, c->order);
     const int grid = grid_for(c, a.chunk * es, cap_fold(c, t, oc, nmax, sched));
-    a.slice = rup(cdiv(a.chunk, grid), vec);
+    a.slice = rup(cdiv(a.chunk, grid), kLLAlign / es);  // whole 128-B lines of LL area per block
     HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
     note_launch(c, a.pv, grid);
     ll_launched(c);
@@ -1287,7 +1304,7 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
     for (int p = 0; p < n; ++p) ptrs[p] = c->stage + p * ustride;
     plan_schedule(c, a, n, root, count, es, ptrs, &nmax, &sched, c->order);
     const int grid = grid_for(c, count * es, cap_fold(c, t, oc, nmax, sched));
-    a.slice = rup(cdiv(count, grid), vec);
+    a.slice = rup(cdiv(count, grid), kLLAlign / es);  // whole 128-B lines of LL area per block
     HIPCK(L(oc, nmax, sched, dim3(grid), c->stream, a));
     note_launch(c, a.pv, grid);
     ll_launched(c);
@@ -1759,7 +1776,11 @@ int knobs_from_env(mpigx_comm* c) {
   // default LL range: 16 KiB — on ranks sharing one GPU the LL step beat the
   // staged one-shot at 8 B but not at 64 KiB (profiles/r02_latency_*); the
   // N>1 bench line measures both at 8 and 64 KiB (MPIGX_ALGO=ll forces LL)
-  c->ll_auto = env_ll("MPIGX_LL_AUTO", 16 << 10);
+  // static default: the staged one-shot (same-device LL measured slower than
+  // it, r03s: 59 vs 32 us at 8 KiB); blocking communicators still time LL
+  // among the candidates of every small size class (mt_cands) and keep it
+  // where it wins on the fabric they run on
+  c->ll_auto = env_ll("MPIGX_LL_AUTO", 0);
   if (c->ll_auto > c->ll_max) c->ll_auto = c->ll_max;
   if (c->ll_auto < 0) c->ll_auto = 0;
   c->ar_tune = env_ll("MPIGX_AR_TUNE", 1) != 0 ? 1 : 0;
@@ -1812,7 +1833,11 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   c->epoch = (uint64_t)env_ll("MPIGX_EPOCH_BASE", 1);  // test hook (LL flag generations); must agree
   if (c->epoch < 1) c->epoch = 1;
   c->ll_gen = (unsigned)(c->epoch >> 31);
-  c->test_import_fail = (int)env_ll("MPIGX_TEST_IMPORT_FAIL", 0);  // per rank: fault injection, not a knob
+  c->test_import_fail = (int)env_ll("MPIGX_TEST_IMPORT_FAIL", 0);
+  c->sig_mode = (int)env_ll("MPIGX_SIG_MODE", 0);  // EXPERIMENT
+  // diagnostic only (selects no path, so not an agreed knob): one stderr line
+  // per launch with its epoch, grid, view key and completion sequence
+  c->diag_trace = env_ll("MPIGX_DIAG_TRACE", 0) != 0;  // per rank: fault injection, not a knob
 
   HIPCK(hipMalloc(&c->stage, c->stage_bytes));
   // rows [0, kMaxBlocks): per-block barriers; row kMaxBlocks: whole-launch
@@ -1903,6 +1928,7 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   me.pci_dev = prop.pciDeviceID;
   me.pci_domain = prop.pciDomainID;
   me.cus = prop.multiProcessorCount;
+  me.max_share = (int)env_ll("MPIGX_MAX_RANKS_PER_DEVICE", 10);
   for (int k = 0; k < MPIGX_KNOB_COUNT; ++k) me.knobs[k] = knob_value(c, k);
   me.epoch0 = c->epoch;
   me.stage_bytes = c->stage_bytes;
@@ -1935,8 +1961,10 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   // dev_share; include/mpigx.h mpigx_comm_device_share)
   {
     int share = 1, cus = me.cus;
+    long long limit_share = me.max_share;
     for (int q = 0; q < nranks; ++q) {
       const ShmRank& a = c->shm->ranks[q];
+      if (a.max_share < limit_share) limit_share = a.max_share;  // every rank applies the same limit
       int k = 0;
       for (int j = 0; j < nranks; ++j) {
         const ShmRank& b = c->shm->ranks[j];
@@ -1947,7 +1975,6 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
     }
     c->dev_share = share;
     c->cus_min = cus;
-    const long long limit_share = env_ll("MPIGX_MAX_RANKS_PER_DEVICE", 10);
     if (share > limit_share) {
       fprintf(stderr,
               "[mpigx] %d ranks share one GPU (limit MPIGX_MAX_RANKS_PER_DEVICE=%lld): more rank processes than "
@@ -2019,6 +2046,19 @@ int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t*
     return rc;
   }
   *out = c;
+  return MPIGX_SUCCESS;
+}
+
+int mpigx_comm_release(mpigx_comm_t c) {
+  // No barrier: every collective kernel's last barrier retires the peers'
+  // accesses to this rank's arena, signal array, LL area and buffers before
+  // it completes here, so once this rank's queued work has drained nothing
+  // of this rank is touched by a peer any more (for the communicator, which
+  // its peers release the same way).
+  if (!c) return MPIGX_ERR_COMM;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  comm_release(c);
   return MPIGX_SUCCESS;
 }
 
@@ -2144,7 +2184,7 @@ int mpigx_comm_ar_costs(mpigx_comm_t c, int* choice, double* ns_per_mib) {
   if (!c) return MPIGX_ERR_COMM;
   if (choice) *choice = c->ar_choice;
   if (ns_per_mib)
-    for (int k = 0; k < 3; ++k) ns_per_mib[k] = c->ar_spb[k] * 1e9 * 1048576.0;
+    for (int k = 0; k < 3; ++k) ns_per_mib[k] = c->ar_spb[k] < 0 ? -1.0 : c->ar_spb[k] * 1e9 * 1048576.0;
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_tune_class(mpigx_comm_t c, int log2_bytes, int* choice, double* ns_per_mib) {
@@ -2197,6 +2237,12 @@ int mpigx_comm_device_share(mpigx_comm_t c, int* ranks, int* cap) {
 int mpigx_comm_set_stamps(mpigx_comm_t c, void* stamps) {
   if (!c) return MPIGX_ERR_COMM;
   c->stamps = (unsigned long long*)stamps;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_set_timeout(mpigx_comm_t c, long long ms) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (ms < 1) return MPIGX_ERR_ARG;
+  c->timeout_ticks = (uint64_t)ms * 100000ull;  // 100 MHz device clock
   return MPIGX_SUCCESS;
 }
 
@@ -2285,7 +2331,7 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
     a.recv = buf;
     if (int e = ll_fill(c, a.pv, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
     const int g = grid_for(c, bytes, cap_copy(c));
-    a.slice = rup(cdiv(bytes, g), 16);
+    a.slice = rup(cdiv(bytes, g), kLLAlign);
     HIPCK(launch_copy(dim3(g), c->stream, a));
     note_launch(c, a.pv, g);
     ll_launched(c);
@@ -2395,7 +2441,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
     a.recv = recv;
     if (int e = ll_fill(c, a.pv, a.ll_push, &a.ll_in, &a.ll_stride, &a.ll_flag)) return e;
     const int g = grid_for(c, bytes, cap_copy(c));
-    a.slice = rup(cdiv(bytes, g), 16);
+    a.slice = rup(cdiv(bytes, g), kLLAlign);
     HIPCK(launch_copy(dim3(g), c->stream, a));
     note_launch(c, a.pv, g);
     ll_launched(c);
@@ -3113,7 +3159,7 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
     a.esize = es;
     a.count = count;
     const int g = grid_for(c, (long long)count * es, cap_scan(c, t, oc));
-    a.slice = rup(cdiv(count, g), vec);
+    a.slice = rup(cdiv(count, g), kLLAlign / es);
     a.send = s;
     a.recv = recvbuf;
     a.ll_ustride = rup(c->ll_max, 16);

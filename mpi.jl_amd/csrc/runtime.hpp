@@ -24,6 +24,7 @@ struct ShmRank {
   int pci_dev;
   int pci_domain;
   int cus;                       // compute units of my device
+  int max_share;                 // MPIGX_MAX_RANKS_PER_DEVICE of this rank (the minimum over ranks applies)
   long long knobs[MPIGX_KNOB_COUNT];  // path-selecting settings read at init (must agree)
   unsigned long long epoch0;          // first barrier epoch (MPIGX_EPOCH_BASE; must agree)
   unsigned long long stage_bytes;
@@ -238,6 +239,8 @@ struct mpigx_comm {
   int bcast_mode = 0;                   // MPIGX_BCAST: 0 auto, 1 direct, 2 sag
   int ring_channels = 1;                // MPIGX_RING_CHANNELS
   unsigned long long* stamps = nullptr; // diagnostic phase timestamps (mpigx_comm_set_stamps)
+  int sig_mode = 0;                     // PeerView.sig_mode (device.hpp sig_put / sig_get)
+  bool diag_trace = false;              // MPIGX_DIAG_TRACE: one stderr line per launch (diagnostic)
   unsigned ll_gen = 0;                  // LL flag generation (epoch >> 31) the LL area was cleared for
   int test_import_fail = 0;             // MPIGX_TEST_IMPORT_FAIL: fail that many peer imports (tests)
   std::mutex mu;

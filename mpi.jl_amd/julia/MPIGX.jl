@@ -67,10 +67,27 @@ const DeviceOrSentinel = Union{ROCBuffer,SentinelPtr}
 # engine communicators, created collectively on first device use of a Comm;
 # the 128-byte unique id travels over host MPI (MPI.Bcast!)
 # ---------------------------------------------------------------------------
-const ENGINE = Dict{Cint,Ptr{Cvoid}}()
+# Keyed by the Comm OBJECT, not its handle value: MPICH hands a freed
+# communicator's handle value to the next new one, which must not inherit a
+# stale engine communicator.  Weak keys: the engine goes with its Comm — a
+# finalizer releases it locally (mpigx_comm_release: no barrier, safe once
+# this rank's last collective on it returned, so a GC finalizer may run it,
+# like comm.jl's finalizer(free, newcomm)); MPI.free(comm) sets comm.val to
+# COMM_NULL, after which engine(comm) refuses the Comm.
+const ENGINE = WeakKeyDict{Comm,Ptr{Cvoid}}()
+
+function _engine_release(comm::Comm)
+    h = pop!(ENGINE, comm, C_NULL)
+    if h != C_NULL
+        ccall((:mpigx_comm_release, libmpigx), Cint, (Ptr{Cvoid},), h)
+        MPI.refcount_dec()
+    end
+    nothing
+end
 
 function engine(comm::Comm)
-    get!(ENGINE, comm.val) do
+    comm.val == MPI.COMM_NULL.val && throw(MPI.MPIError(Cint(5)))  # MPI_ERR_COMM (MPICH mpi.h): a freed Comm
+    get!(ENGINE, comm) do
         id = zeros(UInt8, 128)
         rank = MPI.Comm_rank(comm)
         if rank == 0
@@ -85,7 +102,8 @@ function engine(comm::Comm)
         h = Ref{Ptr{Cvoid}}(C_NULL)
         @mpichk ccall((:mpigx_comm_init_rank, libmpigx), Cint, (Ptr{Ptr{Cvoid}}, Cint, Ptr{UInt8}, Cint, Cint),
                       h, MPI.Comm_size(comm), id, rank, device)
-        MPI.refcount_inc()  # freed (collectively) before MPI_Finalize
+        MPI.refcount_inc()  # released before MPI_Finalize (refcount_dec in _engine_release)
+        comm === MPI.COMM_WORLD || comm === MPI.COMM_SELF || finalizer(_engine_release, comm)
         h[]
     end
 end
@@ -560,11 +578,9 @@ function DeviceOp(f, ::Type{T}; iscommutative=false) where T
 end
 
 function __finalize()
-    for h in values(ENGINE)
-        ccall((:mpigx_comm_free, libmpigx), Cint, (Ptr{Cvoid},), h)
-        MPI.refcount_dec()
+    for comm in collect(keys(ENGINE))
+        _engine_release(comm)
     end
-    empty!(ENGINE)
 end
 # MPI.jl 0.14 has init hooks but no finalize hooks (environment.jl:26-62):
 # engine communicators hold a refcount like any MPI object, so the libmpi

@@ -101,15 +101,24 @@ def main():
     recv = torch.empty_like(send)
     MPI.Allreduce_(send, recv, MPI.SUM, comm)
     xs = [f32_input(q, count, 1000) for q in range(n)]
-    chunk = -(-(-(-count // n)) // 4) * 4
-    spans = [(0, 1 << 16), (count - (1 << 16), count)] + \
-            [(c * chunk - 4096, c * chunk + 4096) for c in range(1, n)] + \
-            [(count // 8 * k - 2048, count // 8 * k + 2048) for k in range(1, 8)]  # Rabenseifner blocks
-    for lo, hi in spans:
-        ins = [x[lo:hi].cpu().numpy() for x in xs]
-        ref = M.fold_rsag(ins, "FLOAT", "SUM")
-        if not np.array_equal(recv[lo:hi].cpu().numpy().view(np.uint32), ref.view(np.uint32)):
-            fails.append(("allreduce-256MiB", lo, hi))
+    # the WHOLE buffer against the oracle: rank r checks the r-th of n equal
+    # parts (f32 SUM's MPICH association depends on the element's position
+    # only through the operand roles, which SUM does not see, so a part folds
+    # like the whole) and every rank's recvbuf must hash like rank 0's (sha1
+    # over the host control plane's gloo group, not through the engine)
+    lo, hi = count * r // n, count * (r + 1) // n
+    ref = M.fold_rsag([x[lo:hi].cpu().numpy() for x in xs], "FLOAT", "SUM")
+    mine = recv[lo:hi].cpu().numpy()
+    if not np.array_equal(mine.view(np.uint32), ref.view(np.uint32)):
+        bad = np.nonzero(mine.view(np.uint32) != ref.view(np.uint32))[0]
+        fails.append(("allreduce-256MiB-whole", lo + int(bad[0]), int(bad.size)))
+    del ref, mine
+    import hashlib
+    import torch.distributed as dist
+    digests = [None] * n
+    dist.all_gather_object(digests, hashlib.sha1(recv.cpu().numpy().tobytes()).hexdigest())
+    if len(set(digests)) != 1:
+        fails.append(("allreduce-256MiB-ranks-differ", digests.index(digests[r])))
     # the same call again (cached zero-copy view) gives the same bits
     again = torch.empty_like(send)
     MPI.Allreduce_(send, again, MPI.SUM, comm)

@@ -12,7 +12,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-env0 = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS": "20000"}
+env0 = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000",
+        "MPIGX_TIMEOUT_MS": os.environ.get("MPIGX_TIMEOUT_MS", "20000")}
 if len(sys.argv) > 2:
     env0["MPIGX_LIB"] = os.path.abspath(sys.argv[2])  # another build of libmpigx.so (A/B)
 s = socket.socket()
@@ -43,7 +44,7 @@ for r, p in enumerate(procs):
     o = open(os.path.join(out_dir, f"scan_repro_r{r}.log")).read()
     lines = [l for l in o.splitlines() if l.startswith("{")]
     prog = [l for l in o.splitlines() if l.startswith(f"r{r} ")]
-    print(f"rank {r} rc={p.returncode} last={prog[-1] if prog else None}", *(lines[-2:] if lines else [o[-800:]]),
+    print(f"rank {r} rc={p.returncode} last={prog[-1] if prog else None}", *(lines[-3:] if lines else [o[-800:]]),
           flush=True)
     if p.returncode and os.environ.get("MPIGX_DIAG_TRACE"):
         ev = [l for l in o.splitlines() if l.startswith("[trace") or l.startswith(f"r{r} ")]
