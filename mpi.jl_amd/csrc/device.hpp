@@ -924,7 +924,8 @@ __device__ __forceinline__ uint64_t sig_get(const uint64_t* slot, int mode) {
 }
 
 __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, int* abort = nullptr,
-                                             unsigned key = 0, bool check_key = false, bool fences = true) {
+                                             unsigned key = 0, bool check_key = false, bool fences = true,
+                                             bool strict = true) {
   __shared__ int s_fail, s_abort;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -965,8 +966,11 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
       }
       // A peer can be at most one barrier ahead of me (it cannot pass this
       // one before my word for it arrived): a word beyond ep + 1 means the
-      // ranks' epochs diverged — fail loudly instead of passing on it.
-      if (ok && (v >> kSigShift) > ep + 1) {
+      // ranks' epochs diverged — fail loudly instead of passing on it.  Not
+      // at the ring's entry (strict = false): a left neighbour runs its ring
+      // steps as soon as ITS left one signals, and its step signals share
+      // my slot for it (kernels.hpp ring_body).
+      if (strict && ok && (v >> kSigShift) > ep + 1) {
         ok = false;
         bad = true;
       }
@@ -1064,9 +1068,9 @@ __device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t e
 // the host in the completion word itself (kernels.hpp signal_done): ONE store
 // carries both "done" and "aborted", so every rank's host reads the same
 // verdict — a separate flag word raced the completion store over PCIe.
-__device__ __forceinline__ bool zc_enter(const PeerView& pv, uint64_t ep, int* abort) {
+__device__ __forceinline__ bool zc_enter(const PeerView& pv, uint64_t ep, int* abort, bool strict = true) {
   *abort = pv.zc_bad;
-  return rank_barrier(pv, ep, abort, pv.zc_key, true);
+  return rank_barrier(pv, ep, abort, pv.zc_key, true, true, strict);
 }
 
 // LL lines of byte messages (common.hpp kLLLine; ll_exchange below):

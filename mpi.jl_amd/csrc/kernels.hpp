@@ -725,7 +725,7 @@ __device__ __forceinline__ int ring_body(const RingArgs& A) {  // returns the ab
   T* recv = (T*)A.zrecv[r];
   uint64_t ep = pv.epoch;
   int ab;
-  if (!zc_enter(pv, ep++, &ab)) return 0;  // every rank's buffers ready, one view
+  if (!zc_enter(pv, ep++, &ab, false)) return 0;  // every rank's buffers ready, one view
   if (!ab) {
     // reduce-scatter: n-1 steps, forward signals ep .. ep+n-2
     for (int s = 0; s < n - 1; ++s) {

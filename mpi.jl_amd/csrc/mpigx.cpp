@@ -375,8 +375,10 @@ int finish(mpigx_comm* c) {
 int kernel_cap(mpigx_comm* c, int occ) {
   const long long share = c->dev_share > 0 ? c->dev_share : 1;
   long long cap;
-  if (share > 1)
+  if (share > 1 && c->share_headroom)
     cap = occ >= 2 ? (long long)c->cus_min * (occ - 1) / share : (long long)c->cus_min * 3 / (4 * share);
+  else if (share > 1)
+    cap = (long long)c->cus_min * (occ >= 6 ? occ - 1 : occ > 0 ? occ : 1) / share;
   else
     cap = (long long)c->cus_min * (occ >= 6 ? occ - 1 : occ > 0 ? occ : 1);
   return (int)(cap < 1 ? 1 : cap > kMaxBlocks ? kMaxBlocks : cap);
@@ -1835,6 +1837,8 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   c->ll_gen = (unsigned)(c->epoch >> 31);
   c->test_import_fail = (int)env_ll("MPIGX_TEST_IMPORT_FAIL", 0);
   c->sig_mode = (int)env_ll("MPIGX_SIG_MODE", 0);  // EXPERIMENT
+  c->share_headroom = env_ll("MPIGX_SHARE_HEADROOM", 1) != 0;  // EXPERIMENT (must agree: grid sizes)
+  c->scan_pp = env_ll("MPIGX_SCAN_PP", 0) != 0;  // EXPERIMENT (must agree: kernel path)
   // diagnostic only (selects no path, so not an agreed knob): one stderr line
   // per launch with its epoch, grid, view key and completion sequence
   c->diag_trace = env_ll("MPIGX_DIAG_TRACE", 0) != 0;  // per rank: fault injection, not a knob
@@ -3112,8 +3116,7 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
   // (and returned wrong words on one rank in another run) while n = 2 and 4
   // were green; cause not found yet.  Its remote stores are the
   // only difference from the pull schedule below, which every test covers.
-  constexpr bool kScanPullPush = false;
-  const bool pp = kScanPullPush && c->n <= 8;
+  const bool pp = c->scan_pp && c->n <= 8;
   if ((pp || sendbuf != MPIGX_IN_PLACE) && c->zc_min > 0 && (long long)count * es >= c->zc_min) {
     // zero-copy: no copy-in, no rounds
     bool staged;

@@ -240,6 +240,8 @@ struct mpigx_comm {
   int ring_channels = 1;                // MPIGX_RING_CHANNELS
   unsigned long long* stamps = nullptr; // diagnostic phase timestamps (mpigx_comm_set_stamps)
   int sig_mode = 0;                     // PeerView.sig_mode (device.hpp sig_put / sig_get)
+  bool share_headroom = true;           // ranks sharing a device leave one block per CU free (kernel_cap)
+  bool scan_pp = false;                 // pull-push Scan / Exscan (kernels.hpp scan_pp_body)
   bool diag_trace = false;              // MPIGX_DIAG_TRACE: one stderr line per launch (diagnostic)
   unsigned ll_gen = 0;                  // LL flag generation (epoch >> 31) the LL area was cleared for
   int test_import_fail = 0;             // MPIGX_TEST_IMPORT_FAIL: fail that many peer imports (tests)

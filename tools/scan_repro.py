@@ -13,7 +13,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "mpi.jl_amd"))
+# REPRO_PKG: another copy of the Python mirror (A/B against an older library)
+sys.path.insert(0, os.environ.get("REPRO_PKG", os.path.join(ROOT, "mpi.jl_amd")))
 
 import torch  # noqa: E402
 

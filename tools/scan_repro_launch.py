@@ -28,10 +28,11 @@ for r in range(n):
                MASTER_PORT=str(port), OMP_NUM_THREADS="1", **env0)
     f = open(os.path.join(out_dir, f"scan_repro_r{r}.log"), "w")
     files.append(f)
-    procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tools", "scan_repro.py")], env=env,
+    script = os.environ.get("REPRO_SCRIPT", os.path.join(ROOT, "tools", "scan_repro.py"))
+    procs.append(subprocess.Popen([sys.executable, "-u", script], env=env,
                                   cwd=ROOT, stdout=f, stderr=subprocess.STDOUT, start_new_session=True))
 t0 = time.time()
-while any(p.poll() is None for p in procs) and time.time() - t0 < 280:
+while any(p.poll() is None for p in procs) and time.time() - t0 < float(os.environ.get("REPRO_WAIT", 280)):
     time.sleep(5)
     print(f"[{time.time() - t0:.0f}s] running: {[r for r, p in enumerate(procs) if p.poll() is None]}", flush=True)
 for p in procs:
