@@ -210,6 +210,18 @@ int mpigx_comm_set_stamps(mpigx_comm_t comm, void *stamps);
  * MPI_ERR_OTHER and the communicator is marked broken (default
  * MPIGX_TIMEOUT_MS, 60000).  Local; applies to later calls.  ms >= 1. */
 int mpigx_comm_set_timeout(mpigx_comm_t comm, long long ms);
+/* Diagnostic: barrier slot row `block` as this rank sees it.  mine[q] = the
+ * word peer q last stored into MY signal array (my own mapping); theirs[q] =
+ * the word I last stored into peer q's array, read back through MY mapping of
+ * it.  A peer whose mine[] entry on its side differs from my theirs[] entry
+ * for it sees another memory than the one I write.  Local. */
+int mpigx_comm_diag_slots(mpigx_comm_t comm, int block, unsigned long long *mine, unsigned long long *theirs);
+/* Diagnostic, COLLECTIVE: every rank writes `nonce` ^ rank into its own
+ * signal arrays (through its own mapping), then reads every peer's through
+ * its IPC mapping of it.  *stale = bitmask of the ranks whose array some rank
+ * (any) saw without the new nonce: that peer's mapping and the owner's no
+ * longer alias one memory.  Every rank gets the same mask. */
+int mpigx_comm_diag_mapcheck(mpigx_comm_t comm, unsigned long long nonce, unsigned *stale);
 /* Zero-copy paths (user buffers mapped by the peers over IPC): how many
  * launches ran on a cached view without any host exchange, and how many
  * host exchanges of buffer registrations there were.  Diagnostic. */

@@ -150,8 +150,24 @@ struct PeerView {
   unsigned long long wbase;
   unsigned long long fbase;
   int sig_mode;                // signal store / poll variant (device.hpp sig_put / sig_get)
-  int pad_;
+  // Two signal arrays and two LL areas per rank (DESIGN §3 "one memory type
+  // per pair"): peers on MY device write into my ordinary (cached, RW)
+  // array, peers on other devices into my uncached one; bit q of rw_mask =
+  // rank q is on my device (my own bit always set).  sig[q] above already
+  // points at the array rank q expects from me.
+  unsigned rw_mask;
+  uint64_t* sig_uc;            // my uncached signal array (cross-device writers)
+  uint64_t* sig_rw;            // my cached signal array (same-device writers and myself)
+  const char* ll_rw;           // my cached LL area at this launch's parity (same-device senders)
 };
+// the array peer `from` writes its words for me into
+__host__ __device__ inline uint64_t* sig_in(const PeerView& pv, int from) {
+  return ((pv.rw_mask >> from) & 1u) ? pv.sig_rw : pv.sig_uc;
+}
+// sender p's LL lines for me at this launch's parity: `in` = my uncached area
+__host__ __device__ inline const char* ll_from(const PeerView& pv, const char* in, int p, long long stride) {
+  return (((pv.rw_mask >> p) & 1u) ? pv.ll_rw : in) + (long long)p * stride;
+}
 
 // Fold-kernel arguments.  Sources/partition are resolved on the host.
 struct FoldArgs {

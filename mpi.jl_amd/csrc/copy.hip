@@ -145,7 +145,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     const uint64_t t0 = wall_clock64();
     for (int p = 0; p < n && ok; ++p) {
       if (p == r) continue;
-      const char* in = A.ll_in + (long long)p * A.ll_stride;
+      const char* in = ll_from(pv, A.ll_in, p, A.ll_stride);
       uint64_t d;
       if (!bc || p == A.root) {
         char* dst = bc ? recv : recv + (long long)p * A.total;

@@ -887,14 +887,20 @@ constexpr unsigned kErrTimeout = 1u, kErrProtocol = 2u;
 // there; the LL two-shot polls between its two pushes.
 __device__ __forceinline__ void flush_remote_stores() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); }
 
-// One pause of a poll loop on a flag / LL line: s_sleep, and every 16th
-// pause a system-scope acquire (L1 + non-coherent L2 invalidate) so that a
-// copy of the polled line cached on this XCD cannot hide a peer's store for
-// longer than ~16 pauses (the stuck rank above polled words its peers had
-// written; this bounds the wait whichever side held the stale copy).
+// One pause of a poll loop on a flag / LL line.  Only s_sleep: the polled
+// words are read with system-scope loads of memory that is uncached in my own
+// mapping (or, between ranks of one device, ordinary memory the hardware
+// keeps coherent), so no cache maintenance is needed to see a peer's store,
+// and the acquire comes once, after the loop.  Round 3 invalidated the L2
+// every 16th pause (buffer_inv sc0 sc1: the whole L2 of the XCD); with 8 ranks
+// on one GPU, spinning blocks then invalidated every XCD's L2 every few
+// hundred cycles while their peers ran ordinary kernels: a 64 Mi-element
+// torch compare took 5.7 s instead of milliseconds, a device synchronize
+// waited a minute, and the stalls looked like lost signal words (r04k).
 __device__ __forceinline__ void spin_pause(unsigned& k) {
-  __builtin_amdgcn_s_sleep(1);
-  if ((++k & 15) == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (k < 64) __builtin_amdgcn_s_sleep(1);  // first ~4 us: tight
+  else __builtin_amdgcn_s_sleep(4);
+  ++k;
 }
 
 // Phase timestamp k of this block (mpigx_comm_set_stamps, diagnostic): one
@@ -940,7 +946,7 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
       const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24) | (uint64_t)(key & 0xffffffu);
       uint64_t* peer_slot = pv.sig[lane] + sig_index(blockIdx.x, pv.rank);
       sig_put(peer_slot, word, mode);
-      uint64_t* mine = pv.sig[pv.rank] + sig_index(blockIdx.x, lane);
+      uint64_t* mine = sig_in(pv, lane) + sig_index(blockIdx.x, lane);
       const uint64_t t0 = wall_clock64();
       uint64_t v;
       unsigned k = 0;
@@ -1035,7 +1041,7 @@ __device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t e
         __hip_atomic_store(pv.sig[lane] + sig_index(row, pv.rank), word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         flush_remote_stores();
       }
-      const uint64_t* mine = pv.sig[pv.rank] + sig_index(row, lane);
+      const uint64_t* mine = sig_in(pv, lane) + sig_index(row, lane);
       const uint64_t t0 = wall_clock64();
       uint64_t v;
       unsigned k = 0;
@@ -1130,9 +1136,9 @@ __device__ __forceinline__ void ll_store8(char* dst, long long i, long long byte
 // I push only after this launch has finished reading (stream order).
 // Returns false (and sets *pv.err) if a sender does not arrive in time.
 // ---------------------------------------------------------------------------
-__device__ __noinline__ bool ll_exchange(char* const* push, const char* in, long long stride, unsigned flag,
-                                         const char* send, long long bytes, long long l0, long long l1, char* unp,
-                                         long long ustride, int n, int r, uint64_t timeout, unsigned* err) {
+__device__ __noinline__ bool ll_exchange(const PeerView& pv, char* const* push, const char* in, long long stride,
+                                         unsigned flag, const char* send, long long bytes, long long l0, long long l1,
+                                         char* unp, long long ustride, int n, int r, uint64_t timeout, unsigned* err) {
   __shared__ int s_ok;
   const long long tid = threadIdx.x, nt = blockDim.x;
   const bool al8 = (((uintptr_t)send) & 7) == 0;
@@ -1162,7 +1168,7 @@ __device__ __noinline__ bool ll_exchange(char* const* push, const char* in, long
   for (long long i = l0 + tid; i < l1 && ok; i += nt) {
     for (int p = 0; p < n && ok; ++p) {
       if (p == r) continue;
-      const uint64_t* q = reinterpret_cast<const uint64_t*>(in + p * stride + kLLLine * i);
+      const uint64_t* q = reinterpret_cast<const uint64_t*>(ll_from(pv, in, p, stride) + kLLLine * i);
       uint64_t a, b;
       unsigned k = 0;
       for (;;) {

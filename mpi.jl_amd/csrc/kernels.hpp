@@ -345,7 +345,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     const long long lo = lmin((long long)b * A.slice, A.count), hi = lmin(lo + A.slice, A.count);
     const long long bytes = A.count * es;
     const long long l0 = (lo * es) / 8, l1 = hi > lo ? (hi * es + 7) / 8 : l0;
-    if (!ll_exchange(A.zc_recv, A.ll_in, A.ll_stride, A.ll_flag, send, bytes, l0, l1, (char*)mine, A.slot_bytes,
+    if (!ll_exchange(pv, A.zc_recv, A.ll_in, A.ll_stride, A.ll_flag, send, bytes, l0, l1, (char*)mine, A.slot_bytes,
                      pv.n, pv.rank, pv.timeout_ticks, pv.err))
       return 0;
     if (A.mode == M_AR_LL || pv.rank == A.root)
@@ -390,7 +390,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       if (p == r) continue;
       for (long long i = rl0 + tid; i < rl1 && ok; i += nt) {
         uint64_t d;
-        ok = ll_get(A.ll_in + (long long)p * A.ll_stride, i, flag, t0, pv.timeout_ticks, &d);
+        ok = ll_get(ll_from(pv, A.ll_in, p, A.ll_stride), i, flag, t0, pv.timeout_ticks, &d);
         if (ok) *reinterpret_cast<uint64_t*>((char*)mine + (long long)p * A.slot_bytes + 8 * i) = d;
       }
     }
@@ -421,7 +421,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       span(p, &c0, &cb, &l0, &l1);
       for (long long i = l0 + tid; i < l1 && ok; i += nt) {
         uint64_t d;
-        ok = ll_get(A.ll_in + (long long)p * A.ll_stride + half, i, flag, t0, pv.timeout_ticks, &d);
+        ok = ll_get(ll_from(pv, A.ll_in, p, A.ll_stride) + half, i, flag, t0, pv.timeout_ticks, &d);
         if (ok) ll_store8((char*)recv + c0 * es, i, cb, d);
       }
     }
@@ -671,7 +671,7 @@ __device__ __forceinline__ void ring_signal(const PeerView& pv, int to, uint64_t
 __device__ __forceinline__ bool ring_wait(const PeerView& pv, int from, uint64_t ep) {
   __shared__ int s_ok;
   if (threadIdx.x == 0) {
-    const uint64_t* slot = pv.sig[pv.rank] + sig_index(blockIdx.x, from);
+    const uint64_t* slot = sig_in(pv, from) + sig_index(blockIdx.x, from);
     const uint64_t t0 = wall_clock64();
     int ok = 1;
     unsigned k = 0;
@@ -1013,7 +1013,7 @@ __device__ __forceinline__ int scan_body(const ScanArgs& A) {  // returns the ab
     // safe), unpacked into my arena slots = src[]; no barrier at all
     const long long es = A.esize, bytes = A.count * es;
     const long long l0 = (lo * es) / 8, l1 = hi > lo ? (hi * es + 7) / 8 : l0;
-    if (!ll_exchange(A.ll_push, A.ll_in, A.ll_stride, A.ll_flag, (const char*)A.send, bytes, l0, l1,
+    if (!ll_exchange(pv, A.ll_push, A.ll_in, A.ll_stride, A.ll_flag, (const char*)A.send, bytes, l0, l1,
                      pv.stage[pv.rank], A.ll_ustride, pv.n, pv.rank, pv.timeout_ticks, pv.err))
       return 0;
   } else if (A.zc) {

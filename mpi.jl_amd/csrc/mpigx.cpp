@@ -256,13 +256,51 @@ namespace {
     }                                                                              \
   } while (0)
 
+int host_allgather(mpigx_comm* c, const void* mine, int len, void* out);
+
+// Ranks sharing a GPU (the test box; one rank per GPU never takes this):
+// before a collective kernel is enqueued, this rank's earlier work on the
+// stream has finished and every rank has got that far (a host barrier over
+// the shm control plane), so the ranks' kernels start together and spin for
+// microseconds.  Without it, ranks that arrived early spin on the device that
+// the late rank's own kernels need: with 8 ranks on one GPU a late rank's
+// torch compare (nonzero) took 5.7 s and a device synchronize over a minute
+// while its peers spun (r04k), and calls timed out.  Blocking communicators
+// only (stream-ordered ones cannot wait); MPIGX_SHARED_GATE=0 disables it.
+int shared_gate(mpigx_comm* c) {
+  if (c->dev_share <= 1 || !c->blocking || !c->shared_gate || c->n == 1) return MPIGX_SUCCESS;
+  HIPCK(hipStreamSynchronize(c->stream));
+  int z = 0, all[kMaxRanks];
+  return host_allgather(c, &z, sizeof z, all);
+}
+
 PeerView make_view(mpigx_comm* c) {
+  if (c->diag_trace) {  // before every launch: the peers' canaries through my mappings of their signal arrays
+    for (int q = 0; q < c->n; ++q) {
+      uint64_t* arr = ((c->rw_mask >> q) & 1u) ? c->peer_sig_rw[q] : c->peer_sig[q];
+      if (q == c->rank || !arr) continue;
+      uint64_t w = 0;
+      void* base = nullptr;
+      size_t size = 0;
+      (void)hipMemcpy(&w, arr + sig_index(kMaxBlocks + 1, 0), sizeof w, hipMemcpyDeviceToHost);
+      (void)hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)arr);
+      (void)hipGetLastError();
+      if (w != (kSigCanary ^ (uint64_t)q) || base != (void*)arr)
+        fprintf(stderr, "[trace r%d] MAPPING of peer %d's signal array at %p: canary %llx (want %llx), "
+                "allocation base %p size %zu\n", c->rank, q, (void*)arr, (unsigned long long)w,
+                (unsigned long long)(kSigCanary ^ (uint64_t)q), base, size);
+    }
+  }
+  // a failed gate (a peer never reached it) breaks the communicator; the
+  // launch that follows then gives up at its first barrier
+  const bool gate_ok = shared_gate(c) == MPIGX_SUCCESS;
+  if (!gate_ok) c->broken = true;
   PeerView pv;
   memset(&pv, 0, sizeof pv);
   pv.rank = c->rank;
   pv.n = c->n;
   pv.epoch = c->epoch;
-  pv.timeout_ticks = c->timeout_ticks;
+  pv.timeout_ticks = gate_ok ? c->timeout_ticks : 0;
   pv.err = c->err_dev;
   pv.done = (c->blocking && c->sync_mode == 1) ? c->done_dev : nullptr;
   pv.dcount = c->dcount_dev;
@@ -272,8 +310,14 @@ PeerView make_view(mpigx_comm* c) {
   pv.seq = c->launch_seq + 1;
   pv.stamps = c->stamps;
   pv.sig_mode = c->sig_mode;
+  // each peer gets its words in the array of ITS memory type for me: ordinary
+  // memory between ranks of one device, uncached across devices (one memory
+  // type per writer / reader pair)
+  pv.rw_mask = c->rw_mask;
+  pv.sig_uc = c->sig;
+  pv.sig_rw = c->sig_rw;
   for (int p = 0; p < c->n; ++p) {
-    pv.sig[p] = c->peer_sig[p];
+    pv.sig[p] = ((c->rw_mask >> p) & 1u) ? c->peer_sig_rw[p] : c->peer_sig[p];
     pv.stage[p] = c->peer_stage[p];
   }
   return pv;
@@ -492,6 +536,9 @@ bool zc_export(mpigx_comm* c, const void* p, char** pbase, unsigned long long* i
   }
   if (c->lreg.size() >= kZcCache) c->lreg.erase(c->lreg.begin());
   c->lreg.push_back({bid, (char*)base, hh});
+  if (c->diag_trace)
+    fprintf(stderr, "[trace r%d] export base=%p size=%zu end=%p id=%llu\n", c->rank, base, size,
+            (char*)base + size, bid);
   *h = hh;
   return true;
 }
@@ -528,6 +575,7 @@ char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemH
     }
   }
   c->imports.push_back({peer, id, (char*)ptr, ++c->tick, 0, h});
+  if (c->diag_trace) fprintf(stderr, "[trace r%d] zc import peer %d id=%llu at %p\n", c->rank, peer, id, ptr);
   return (char*)ptr;
 }
 
@@ -1001,7 +1049,8 @@ int ll_fill(mpigx_comm* c, PeerView& pv, char** push, const char** in, long long
   if ((unsigned)(c->epoch >> 31) != c->ll_gen) {
     int rc = barrier_launch(c);
     if (rc) return rc;
-    HIPCK(hipMemsetAsync(c->ll, 0, (size_t)2 * kMaxRanks * c->ll_stride, c->stream));
+    if (c->ll) HIPCK(hipMemsetAsync(c->ll, 0, (size_t)2 * kMaxRanks * c->ll_stride, c->stream));
+    if (c->ll_rw) HIPCK(hipMemsetAsync(c->ll_rw, 0, (size_t)2 * kMaxRanks * c->ll_stride, c->stream));
     if ((rc = barrier_launch(c))) return rc;
     c->ll_gen = (unsigned)(c->epoch >> 31);
     const unsigned key = pv.zc_key;
@@ -1011,8 +1060,12 @@ int ll_fill(mpigx_comm* c, PeerView& pv, char** push, const char** in, long long
     pv.zc_bad = bad;
   }
   const long long par = (long long)(c->ll_seq & 1) * kMaxRanks * c->ll_stride;
-  for (int p = 0; p < c->n; ++p) push[p] = c->peer_ll[p] + par + (long long)c->rank * c->ll_stride;
-  *in = c->ll + par;
+  for (int p = 0; p < c->n; ++p) {
+    char* area = ((c->rw_mask >> p) & 1u) ? c->peer_ll_rw[p] : c->peer_ll[p];
+    push[p] = area ? area + par + (long long)c->rank * c->ll_stride : nullptr;
+  }
+  *in = c->ll ? c->ll + par : nullptr;
+  pv.ll_rw = c->ll_rw ? c->ll_rw + par : nullptr;
   *stride = c->ll_stride;
   *flag = (unsigned)(c->epoch & 0x7fffffffu) | 0x80000000u;
   return MPIGX_SUCCESS;
@@ -1807,6 +1860,10 @@ void comm_release(mpigx_comm* c) {
     if (c->peer_opened[q]) (void)hipIpcCloseMemHandle(c->peer_stage[q]);
     if (c->peer_sig_opened[q]) (void)hipIpcCloseMemHandle(c->peer_sig[q]);
     if (c->peer_ll_opened[q]) (void)hipIpcCloseMemHandle(c->peer_ll[q]);
+    if (c->peer_rw_opened[q]) {
+      (void)hipIpcCloseMemHandle(c->peer_sig_rw[q]);
+      if (c->peer_ll_rw[q]) (void)hipIpcCloseMemHandle(c->peer_ll_rw[q]);
+    }
   }
   for (auto& im : c->imports) (void)hipIpcCloseMemHandle(im.base);
   if (c->shm) munmap(c->shm, sizeof(ShmBlock));
@@ -1814,7 +1871,9 @@ void comm_release(mpigx_comm* c) {
   for (auto& b : c->tmp_used) (void)hipFree(b.second);
   if (c->stage) (void)hipFree(c->stage);
   if (c->sig) (void)hipFree(c->sig);
+  if (c->sig_rw) (void)hipFree(c->sig_rw);
   if (c->ll) (void)hipFree(c->ll);
+  if (c->ll_rw) (void)hipFree(c->ll_rw);
   if (c->dcount_dev) (void)hipFree(c->dcount_dev);
   for (auto& e : c->ar_ev)
     if (e) (void)hipEventDestroy(e);
@@ -1839,6 +1898,8 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   c->sig_mode = (int)env_ll("MPIGX_SIG_MODE", 0);  // EXPERIMENT
   c->share_headroom = env_ll("MPIGX_SHARE_HEADROOM", 1) != 0;  // EXPERIMENT (must agree: grid sizes)
   c->scan_pp = env_ll("MPIGX_SCAN_PP", 0) != 0;  // EXPERIMENT (must agree: kernel path)
+  c->sig_pair = env_ll("MPIGX_SIG_PAIR", 1) != 0;  // EXPERIMENT: 0 = every peer writes my uncached arrays
+  c->shared_gate = env_ll("MPIGX_SHARED_GATE", 1) != 0;  // ranks sharing a GPU: host gate before launches
   // diagnostic only (selects no path, so not an agreed knob): one stderr line
   // per launch with its epoch, grid, view key and completion sequence
   c->diag_trace = env_ll("MPIGX_DIAG_TRACE", 0) != 0;  // per rank: fault injection, not a knob
@@ -1846,12 +1907,31 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   HIPCK(hipMalloc(&c->stage, c->stage_bytes));
   // rows [0, kMaxBlocks): per-block barriers; row kMaxBlocks: whole-launch
   // barrier (device.hpp rank_barrier_grid)
-  const size_t sig_bytes = sig_index(kMaxBlocks + 1, 0) * sizeof(uint64_t);
+  // + one row: word 0 of row kMaxBlocks + 1 holds this rank's canary
+  // (kSigCanary ^ rank), which the launch trace reads through every peer's
+  // mapping to check that the mapping still aliases the peer's array
+  // Two of each (DESIGN §3 "one memory type per writer / reader pair"): a
+  // peer on ANOTHER device stores into my uncached array (its mapping of my
+  // memory reaches HBM over xGMI, my polls read HBM); a peer on MY device
+  // stores into my ordinary-memory array.  Its IPC import of my memory is an
+  // ordinary cached mapping whatever my allocation's flags, so a store it
+  // makes into my UNCACHED array stays a dirty line in its XCD's L2 that its
+  // release does not write back and my uncached polls never see (8 ranks on
+  // one GPU: the root's entry word never reached rank 0; an atomic read of
+  // the slot on rank 0 saw the old word too, r04e/r04h) — between two
+  // cached mappings of ordinary memory the hardware keeps the XCDs' L2s
+  // coherent as within one process.
+  const size_t sig_bytes = sig_index(kMaxBlocks + 2, 0) * sizeof(uint64_t);
   HIPCK(hipExtMallocWithFlags((void**)&c->sig, sig_bytes, hipDeviceMallocUncached));
+  HIPCK(hipMalloc((void**)&c->sig_rw, sig_bytes));
   HIPCK(hipMemset(c->sig, 0, sig_bytes));
-  // LL area for small messages (M_AR_LL ...): uncached like the signal array,
-  // so peers' 64-bit line stores and my polls meet in HBM with no cache in
-  // between
+  HIPCK(hipMemset(c->sig_rw, 0, sig_bytes));
+  {
+    const uint64_t canary = kSigCanary ^ (uint64_t)rank;
+    HIPCK(hipMemcpy(c->sig + sig_index(kMaxBlocks + 1, 0), &canary, sizeof canary, hipMemcpyHostToDevice));
+    HIPCK(hipMemcpy(c->sig_rw + sig_index(kMaxBlocks + 1, 0), &canary, sizeof canary, hipMemcpyHostToDevice));
+  }
+  // LL areas for small messages (M_AR_LL ...): the same two memory types
   c->ll_stride = rup(c->ll_max, 16) / 8 * kLLLine;
   // events of the measured algorithm choices (MPIGX_AR_TUNE)
   for (auto& x : c->mt_choice) x = -1;
@@ -1862,7 +1942,9 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   if (c->ll_max > 0 && nranks > 1) {
     const size_t llb = (size_t)2 * kMaxRanks * c->ll_stride;
     HIPCK(hipExtMallocWithFlags((void**)&c->ll, llb, hipDeviceMallocUncached));
+    HIPCK(hipMalloc((void**)&c->ll_rw, llb));
     HIPCK(hipMemset(c->ll, 0, llb));
+    HIPCK(hipMemset(c->ll_rw, 0, llb));
   }
   HIPCK(hipHostMalloc((void**)&c->err, 64, hipHostMallocCoherent | hipHostMallocMapped));
   memset(c->err, 0, 64);
@@ -1875,6 +1957,9 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   c->peer_stage[rank] = c->stage;
   c->peer_sig[rank] = c->sig;
   c->peer_ll[rank] = c->ll;
+  c->peer_sig_rw[rank] = c->sig_rw;
+  c->peer_ll_rw[rank] = c->ll_rw;
+  c->rw_mask = 1u << rank;
   {
     int cus = 0;
     HIPCK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -1938,11 +2023,15 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   me.stage_bytes = c->stage_bytes;
   me.stage_ptr = (unsigned long long)(uintptr_t)c->stage;
   me.sig_ptr = (unsigned long long)(uintptr_t)c->sig;
+  me.sig_rw_ptr = (unsigned long long)(uintptr_t)c->sig_rw;
   HIPCK(hipIpcGetMemHandle(&me.stage_h, c->stage));
   HIPCK(hipIpcGetMemHandle(&me.sig_h, c->sig));
+  HIPCK(hipIpcGetMemHandle(&me.sig_rw_h, c->sig_rw));
   me.ll_bytes = c->ll ? (unsigned long long)c->ll_max : 0;
   me.ll_ptr = (unsigned long long)(uintptr_t)c->ll;
+  me.ll_rw_ptr = (unsigned long long)(uintptr_t)c->ll_rw;
   if (c->ll) HIPCK(hipIpcGetMemHandle(&me.ll_h, c->ll));
+  if (c->ll_rw) HIPCK(hipIpcGetMemHandle(&me.ll_rw_h, c->ll_rw));
   c->shm->arrived.fetch_add(1, std::memory_order_acq_rel);
   while (c->shm->arrived.load(std::memory_order_acquire) < nranks) {
     if (now_s() - t0 > limit) return MPIGX_ERR_OTHER;
@@ -1991,25 +2080,42 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
     if (q == rank) continue;
     const ShmRank& pr = c->shm->ranks[q];
     c->same_device[q] = pr.pci_domain == me.pci_domain && pr.pci_bus == me.pci_bus && pr.pci_dev == me.pci_dev;
+    if (c->same_device[q] && c->sig_pair) c->rw_mask |= 1u << q;
     if (pr.pid == me.pid) {
       c->peer_stage[q] = (char*)(uintptr_t)pr.stage_ptr;
       c->peer_sig[q] = (uint64_t*)(uintptr_t)pr.sig_ptr;
       c->peer_ll[q] = (char*)(uintptr_t)pr.ll_ptr;
+      c->peer_sig_rw[q] = (uint64_t*)(uintptr_t)pr.sig_rw_ptr;
+      c->peer_ll_rw[q] = (char*)(uintptr_t)pr.ll_rw_ptr;
     } else {
       void* ps = nullptr;
-      void* pg = nullptr;
       HIPCK(hipIpcOpenMemHandle(&ps, pr.stage_h, hipIpcMemLazyEnablePeerAccess));
       c->peer_stage[q] = (char*)ps;
       c->peer_opened[q] = true;
-      HIPCK(hipIpcOpenMemHandle(&pg, pr.sig_h, hipIpcMemLazyEnablePeerAccess));
-      c->peer_sig[q] = (uint64_t*)pg;
-      c->peer_sig_opened[q] = true;
-      if (c->ll) {
-        void* pl = nullptr;
-        HIPCK(hipIpcOpenMemHandle(&pl, pr.ll_h, hipIpcMemLazyEnablePeerAccess));
-        c->peer_ll[q] = (char*)pl;
-        c->peer_ll_opened[q] = true;
+      // only the signal array / LL area of the memory type this pair uses
+      void* pg = nullptr;
+      void* pl = nullptr;
+      if ((c->rw_mask >> q) & 1u) {
+        HIPCK(hipIpcOpenMemHandle(&pg, pr.sig_rw_h, hipIpcMemLazyEnablePeerAccess));
+        c->peer_sig_rw[q] = (uint64_t*)pg;
+        c->peer_rw_opened[q] = true;
+        if (c->ll) {
+          HIPCK(hipIpcOpenMemHandle(&pl, pr.ll_rw_h, hipIpcMemLazyEnablePeerAccess));
+          c->peer_ll_rw[q] = (char*)pl;
+        }
+      } else {
+        HIPCK(hipIpcOpenMemHandle(&pg, pr.sig_h, hipIpcMemLazyEnablePeerAccess));
+        c->peer_sig[q] = (uint64_t*)pg;
+        c->peer_sig_opened[q] = true;
+        if (c->ll) {
+          HIPCK(hipIpcOpenMemHandle(&pl, pr.ll_h, hipIpcMemLazyEnablePeerAccess));
+          c->peer_ll[q] = (char*)pl;
+          c->peer_ll_opened[q] = true;
+        }
       }
+      if (c->diag_trace)
+        fprintf(stderr, "[trace r%d] import peer %d (%s) sig=%p ll=%p stage=%p\n", rank, q,
+                c->same_device[q] ? "same device: ordinary memory" : "other device: uncached", pg, pl, ps);
     }
   }
   c->shm->connected.fetch_add(1, std::memory_order_acq_rel);
@@ -2241,6 +2347,50 @@ int mpigx_comm_device_share(mpigx_comm_t c, int* ranks, int* cap) {
 int mpigx_comm_set_stamps(mpigx_comm_t c, void* stamps) {
   if (!c) return MPIGX_ERR_COMM;
   c->stamps = (unsigned long long*)stamps;
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_diag_slots(mpigx_comm_t c, int block, unsigned long long* mine, unsigned long long* theirs) {
+  if (!c) return MPIGX_ERR_COMM;
+  if (block < 0 || block > kMaxBlocks || !mine || !theirs) return MPIGX_ERR_ARG;
+  (void)hipSetDevice(c->device);
+  for (int q = 0; q < c->n; ++q) {
+    mine[q] = theirs[q] = 0;
+    const bool rw = (c->rw_mask >> q) & 1u;
+    if (hipMemcpy(&mine[q], (rw ? c->sig_rw : c->sig) + sig_index(block, q), 8, hipMemcpyDeviceToHost) !=
+            hipSuccess ||
+        hipMemcpy(&theirs[q], (rw ? c->peer_sig_rw[q] : c->peer_sig[q]) + sig_index(block, c->rank), 8,
+                  hipMemcpyDeviceToHost) != hipSuccess) {
+      (void)hipGetLastError();
+      return MPIGX_ERR_INTERN;
+    }
+  }
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_diag_mapcheck(mpigx_comm_t c, unsigned long long nonce, unsigned* stale) {
+  if (!c || !stale) return MPIGX_ERR_COMM;
+  *stale = 0;
+  if (c->n == 1) return MPIGX_SUCCESS;
+  (void)hipSetDevice(c->device);
+  HIPCK(hipStreamSynchronize(c->stream));
+  const uint64_t mine = nonce ^ (uint64_t)c->rank;
+  const size_t at = sig_index(kMaxBlocks + 1, 0);
+  HIPCK(hipMemcpy(c->sig + at, &mine, 8, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(c->sig_rw + at, &mine, 8, hipMemcpyHostToDevice));
+  int dummy = 0, all_dummy[kMaxRanks];
+  int rc = host_allgather(c, &dummy, sizeof dummy, all_dummy);  // every rank has written
+  if (rc) return rc;
+  unsigned seen_stale = 0;
+  for (int q = 0; q < c->n; ++q) {
+    if (q == c->rank) continue;
+    uint64_t* arr = ((c->rw_mask >> q) & 1u) ? c->peer_sig_rw[q] : c->peer_sig[q];
+    uint64_t w = 0;
+    HIPCK(hipMemcpy(&w, arr + at, 8, hipMemcpyDeviceToHost));
+    if (w != (nonce ^ (uint64_t)q)) seen_stale |= 1u << q;
+  }
+  unsigned all[kMaxRanks];
+  rc = host_allgather(c, &seen_stale, sizeof seen_stale, all);
+  if (rc) return rc;
+  for (int q = 0; q < c->n; ++q) *stale |= all[q];
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_set_timeout(mpigx_comm_t c, long long ms) {

@@ -17,6 +17,8 @@ namespace mpigx {
 // ---------------------------------------------------------------------------
 constexpr uint64_t kMagic = 0x6d70696778763034ull;  // "mpigxv04"
 
+constexpr uint64_t kSigCanary = 0x6d70696778c0ffeeull;  // signal-array canary (mpigx.cpp comm_init)
+
 struct ShmRank {
   int pid;
   int device;
@@ -30,8 +32,12 @@ struct ShmRank {
   unsigned long long stage_bytes;
   unsigned long long stage_ptr;  // raw pointer (same-process peers)
   unsigned long long sig_ptr;
+  unsigned long long sig_rw_ptr;
+  unsigned long long ll_rw_ptr;
   hipIpcMemHandle_t stage_h;
   hipIpcMemHandle_t sig_h;
+  hipIpcMemHandle_t sig_rw_h;
+  hipIpcMemHandle_t ll_rw_h;
   unsigned long long ll_bytes;   // LL area size (0: none; must agree on every rank)
   unsigned long long ll_ptr;
   hipIpcMemHandle_t ll_h;
@@ -129,8 +135,11 @@ struct mpigx_comm {
   // local resources
   char* stage = nullptr;
   size_t stage_bytes = 0;
-  uint64_t* sig = nullptr;
+  uint64_t* sig = nullptr;     // signal array, uncached: words from peers on OTHER devices
+  uint64_t* sig_rw = nullptr;  // signal array, ordinary memory: words from peers on MY device (and mine)
   char* ll = nullptr;          // LL area (uncached): [2 parities][kMaxRanks senders][ll_stride]
+  char* ll_rw = nullptr;       // LL area, ordinary memory: lines from peers on my device
+  unsigned rw_mask = 0;        // bit q: rank q is on my device (bit rank always set)
   long long ll_max = 0;        // MPIGX_LL_MAX: LL capacity per sender (bytes; 0: no LL area)
   long long ll_auto = 0;       // MPIGX_LL_AUTO: largest message that takes LL by default
   long long ll_stride = 0;     // bytes of one sender's lines (2 x ll_max rounded to 16)
@@ -216,6 +225,9 @@ struct mpigx_comm {
   // peers (index = rank; self included)
   char* peer_stage[mpigx::kMaxRanks] = {};
   uint64_t* peer_sig[mpigx::kMaxRanks] = {};
+  uint64_t* peer_sig_rw[mpigx::kMaxRanks] = {};  // every rank's ordinary-memory signal array (IPC-mapped)
+  char* peer_ll_rw[mpigx::kMaxRanks] = {};
+  bool peer_rw_opened[mpigx::kMaxRanks] = {};
   bool peer_opened[mpigx::kMaxRanks] = {};      // peer_stage[q] is an IPC mapping of ours
   bool peer_sig_opened[mpigx::kMaxRanks] = {};  // peer_sig[q] likewise
   char* peer_ll[mpigx::kMaxRanks] = {};         // every rank's LL area (IPC-mapped)
@@ -241,7 +253,9 @@ struct mpigx_comm {
   unsigned long long* stamps = nullptr; // diagnostic phase timestamps (mpigx_comm_set_stamps)
   int sig_mode = 0;                     // PeerView.sig_mode (device.hpp sig_put / sig_get)
   bool share_headroom = true;           // ranks sharing a device leave one block per CU free (kernel_cap)
-  bool scan_pp = false;                 // pull-push Scan / Exscan (kernels.hpp scan_pp_body)
+  bool scan_pp = false;
+  bool sig_pair = true;
+  bool shared_gate = true;              // mpigx.cpp shared_gate                 // same-device peers use my ordinary-memory arrays                 // pull-push Scan / Exscan (kernels.hpp scan_pp_body)
   bool diag_trace = false;              // MPIGX_DIAG_TRACE: one stderr line per launch (diagnostic)
   unsigned ll_gen = 0;                  // LL flag generation (epoch >> 31) the LL area was cleared for
   int test_import_fail = 0;             // MPIGX_TEST_IMPORT_FAIL: fail that many peer imports (tests)

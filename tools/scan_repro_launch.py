@@ -45,7 +45,7 @@ for r, p in enumerate(procs):
     o = open(os.path.join(out_dir, f"scan_repro_r{r}.log")).read()
     lines = [l for l in o.splitlines() if l.startswith("{")]
     prog = [l for l in o.splitlines() if l.startswith(f"r{r} ")]
-    print(f"rank {r} rc={p.returncode} last={prog[-1] if prog else None}", *(lines[-3:] if lines else [o[-800:]]),
+    print(f"rank {r} rc={p.returncode} last={prog[-1] if prog else None}", *(lines[-4:] if lines else [o[-800:]]),
           flush=True)
     if p.returncode and os.environ.get("MPIGX_DIAG_TRACE"):
         ev = [l for l in o.splitlines() if l.startswith("[trace") or l.startswith(f"r{r} ")]
