@@ -149,7 +149,6 @@ struct PeerView {
   // this launch
   unsigned long long wbase;
   unsigned long long fbase;
-  int sig_mode;                // signal store / poll variant (device.hpp sig_put / sig_get)
   // Two signal arrays and two LL areas per rank (DESIGN §3 "one memory type
   // per pair"): peers on MY device write into my ordinary (cached, RW)
   // array, peers on other devices into my uncached one; bit q of rw_mask =

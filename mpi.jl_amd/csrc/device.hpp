@@ -916,16 +916,13 @@ __device__ __forceinline__ uint64_t opaque_zero() {
   asm volatile("" : "+v"(z));
   return z;
 }
-// Signal word into a peer's slot (sig_mode bit 0: atomic swap instead of a
-// store), and a poll of my own slot (bit 2: read-modify-write read).
-__device__ __forceinline__ void sig_put(uint64_t* slot, uint64_t word, int mode) {
-  if (mode & 1) (void)__hip_atomic_exchange(slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else __hip_atomic_store(slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// Signal word into a peer's slot, then written back out of this XCD's L2
+// (flush_remote_stores); a poll of my own slot.
+__device__ __forceinline__ void sig_put(uint64_t* slot, uint64_t word) {
+  __hip_atomic_store(slot, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   flush_remote_stores();
 }
-__device__ __forceinline__ uint64_t sig_get(const uint64_t* slot, int mode) {
-  if (mode & 4) return __hip_atomic_fetch_add(const_cast<uint64_t*>(slot), opaque_zero(), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint64_t sig_get(const uint64_t* slot) {
   return __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -942,17 +939,15 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bool ok = true, ab = false, bad = false;
     if (lane < pv.n) {
-      const int mode = pv.sig_mode;
       const uint64_t word = (ep << kSigShift) | ((uint64_t)(ab_in ? 1 : 0) << 24) | (uint64_t)(key & 0xffffffu);
       uint64_t* peer_slot = pv.sig[lane] + sig_index(blockIdx.x, pv.rank);
-      sig_put(peer_slot, word, mode);
+      sig_put(peer_slot, word);
       uint64_t* mine = sig_in(pv, lane) + sig_index(blockIdx.x, lane);
       const uint64_t t0 = wall_clock64();
       uint64_t v;
       unsigned k = 0;
-      while (((v = sig_get(mine, mode)) >> kSigShift) < ep) {
+      while (((v = sig_get(mine)) >> kSigShift) < ep) {
         spin_pause(k);
-        if ((mode & 2) && (k & 63) == 0) sig_put(peer_slot, word, mode);  // republish my word
         if (wall_clock64() - t0 > pv.timeout_ticks) {
           ok = false;
           if (pv.stamps) {  // diagnostic: the epoch awaited and the word last seen from that peer

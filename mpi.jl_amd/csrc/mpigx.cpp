@@ -309,7 +309,6 @@ PeerView make_view(mpigx_comm* c) {
   pv.fbase = c->wfinished;
   pv.seq = c->launch_seq + 1;
   pv.stamps = c->stamps;
-  pv.sig_mode = c->sig_mode;
   // each peer gets its words in the array of ITS memory type for me: ordinary
   // memory between ranks of one device, uncached across devices (one memory
   // type per writer / reader pair)
@@ -1895,10 +1894,8 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   if (c->epoch < 1) c->epoch = 1;
   c->ll_gen = (unsigned)(c->epoch >> 31);
   c->test_import_fail = (int)env_ll("MPIGX_TEST_IMPORT_FAIL", 0);
-  c->sig_mode = (int)env_ll("MPIGX_SIG_MODE", 0);  // EXPERIMENT
   c->share_headroom = env_ll("MPIGX_SHARE_HEADROOM", 1) != 0;  // EXPERIMENT (must agree: grid sizes)
   c->scan_pp = env_ll("MPIGX_SCAN_PP", 0) != 0;  // EXPERIMENT (must agree: kernel path)
-  c->sig_pair = env_ll("MPIGX_SIG_PAIR", 1) != 0;  // EXPERIMENT: 0 = every peer writes my uncached arrays
   c->shared_gate = env_ll("MPIGX_SHARED_GATE", 1) != 0;  // ranks sharing a GPU: host gate before launches
   // diagnostic only (selects no path, so not an agreed knob): one stderr line
   // per launch with its epoch, grid, view key and completion sequence
@@ -2080,7 +2077,7 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
     if (q == rank) continue;
     const ShmRank& pr = c->shm->ranks[q];
     c->same_device[q] = pr.pci_domain == me.pci_domain && pr.pci_bus == me.pci_bus && pr.pci_dev == me.pci_dev;
-    if (c->same_device[q] && c->sig_pair) c->rw_mask |= 1u << q;
+    if (c->same_device[q]) c->rw_mask |= 1u << q;
     if (pr.pid == me.pid) {
       c->peer_stage[q] = (char*)(uintptr_t)pr.stage_ptr;
       c->peer_sig[q] = (uint64_t*)(uintptr_t)pr.sig_ptr;
