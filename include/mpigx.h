@@ -173,7 +173,12 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
 #define MPIGX_KNOB_AR_SLICES 15       /* MPIGX_AR_SLICES: pull-push two-shot / zero-copy Reduce slices per
                                          block handed out dynamically (0, default: one static slice per
                                          block; 1-64) */
-#define MPIGX_KNOB_COUNT 16
+#define MPIGX_KNOB_SCAN_PP 16        /* MPIGX_SCAN_PP: 0/1, pull-push Scan / Exscan at n <= 8 (default 1) */
+#define MPIGX_KNOB_SHARE_HEADROOM 17 /* MPIGX_SHARE_HEADROOM: 0/1, ranks sharing a GPU leave one block per CU
+                                        free in the spinning kernels' grid caps (default 0) */
+#define MPIGX_KNOB_SHARED_GATE 18    /* MPIGX_SHARED_GATE: 0/1, ranks sharing a GPU drain their stream and meet
+                                        on the host before each collective launch (default 1) */
+#define MPIGX_KNOB_COUNT 19
 #define MPIGX_ALGO_AUTO 0     /* unset: static rules + the measured choices */
 #define MPIGX_ALGO_LL 1       /* "ll" */
 #define MPIGX_ALGO_LL2 2      /* "ll2" */

@@ -1680,7 +1680,7 @@ const char* const kKnobEnv[MPIGX_KNOB_COUNT] = {
     "MPIGX_ALGO",   "MPIGX_BCAST",      "MPIGX_RING_CHANNELS", "MPIGX_MAX_BLOCKS",     "MPIGX_ONESHOT_MAX",
     "MPIGX_ZC_MIN", "MPIGX_BCAST_SAG_MIN", "MPIGX_ZC_REQUIRE", "MPIGX_BYTES_PER_BLOCK", "MPIGX_LL_AUTO",
     "MPIGX_AR_TUNE", "MPIGX_ZC_OPTIMISTIC", "MPIGX_SYNC_SPIN", "MPIGX_STAGING_BYTES",  "MPIGX_LL_MAX",
-    "MPIGX_AR_SLICES"};
+    "MPIGX_AR_SLICES", "MPIGX_SCAN_PP", "MPIGX_SHARE_HEADROOM", "MPIGX_SHARED_GATE"};
 
 long long knob_value(const mpigx_comm* c, int k) {
   switch (k) {
@@ -1700,6 +1700,9 @@ long long knob_value(const mpigx_comm* c, int k) {
     case MPIGX_KNOB_STAGING_BYTES: return (long long)c->stage_bytes;
     case MPIGX_KNOB_LL_MAX: return c->ll_max;
     case MPIGX_KNOB_AR_SLICES: return c->ar_slices;
+    case MPIGX_KNOB_SCAN_PP: return c->scan_pp ? 1 : 0;
+    case MPIGX_KNOB_SHARE_HEADROOM: return c->share_headroom ? 1 : 0;
+    case MPIGX_KNOB_SHARED_GATE: return c->shared_gate ? 1 : 0;
     default: return -1;
   }
 }
@@ -1778,6 +1781,18 @@ int knob_apply(mpigx_comm* c, int k, long long v, bool init) {
       if (!in(0, 64)) return MPIGX_ERR_ARG;
       c->ar_slices = (int)v;
       return MPIGX_SUCCESS;
+    case MPIGX_KNOB_SCAN_PP:
+      if (!in(0, 1)) return MPIGX_ERR_ARG;
+      c->scan_pp = v != 0;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_SHARE_HEADROOM:
+      if (!in(0, 1)) return MPIGX_ERR_ARG;
+      c->share_headroom = v != 0;
+      return MPIGX_SUCCESS;
+    case MPIGX_KNOB_SHARED_GATE:
+      if (!in(0, 1)) return MPIGX_ERR_ARG;
+      c->shared_gate = v != 0;
+      return MPIGX_SUCCESS;
     default: return MPIGX_ERR_ARG;
   }
 }
@@ -1827,9 +1842,6 @@ int knobs_from_env(mpigx_comm* c) {
   c->ll_max = env_ll("MPIGX_LL_MAX", 256 << 10);
   if (c->ll_max < 0) c->ll_max = 0;
   if (c->ll_max > (4ll << 20)) c->ll_max = 4ll << 20;
-  // default LL range: 16 KiB — on ranks sharing one GPU the LL step beat the
-  // staged one-shot at 8 B but not at 64 KiB (profiles/r02_latency_*); the
-  // N>1 bench line measures both at 8 and 64 KiB (MPIGX_ALGO=ll forces LL)
   // static default: the staged one-shot (same-device LL measured slower than
   // it, r03s: 59 vs 32 us at 8 KiB); blocking communicators still time LL
   // among the candidates of every small size class (mt_cands) and keep it
@@ -1844,6 +1856,15 @@ int knobs_from_env(mpigx_comm* c) {
   // moved the straggler tail but not the span (profiles/r03e_coll_n2_1gpu.json)
   const long long sl = env_ll("MPIGX_AR_SLICES", 0);
   c->ar_slices = (int)(sl < 0 ? 0 : sl > 64 ? 64 : sl);
+  // pull-push Scan / Exscan: on since round 4 (the round-3 n = 8 fault did
+  // not recur with the kernel's checked preconditions: the GPU suite with it
+  // forced and the 8-rank headline / sequence / large-count cases, r04n)
+  c->scan_pp = env_ll("MPIGX_SCAN_PP", 1) != 0;
+  // no residency headroom since round 4: the n = 8 cases pass without it and
+  // the same-device pull-push kernel takes 270 us at 256 blocks against 285
+  // at 128 (r04n coll_prof); MPIGX_SHARE_HEADROOM=1 restores it
+  c->share_headroom = env_ll("MPIGX_SHARE_HEADROOM", 0) != 0;
+  c->shared_gate = env_ll("MPIGX_SHARED_GATE", 1) != 0;
   return MPIGX_SUCCESS;
 }
 
@@ -1894,9 +1915,6 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   if (c->epoch < 1) c->epoch = 1;
   c->ll_gen = (unsigned)(c->epoch >> 31);
   c->test_import_fail = (int)env_ll("MPIGX_TEST_IMPORT_FAIL", 0);
-  c->share_headroom = env_ll("MPIGX_SHARE_HEADROOM", 1) != 0;  // EXPERIMENT (must agree: grid sizes)
-  c->scan_pp = env_ll("MPIGX_SCAN_PP", 0) != 0;  // EXPERIMENT (must agree: kernel path)
-  c->shared_gate = env_ll("MPIGX_SHARED_GATE", 1) != 0;  // ranks sharing a GPU: host gate before launches
   // diagnostic only (selects no path, so not an agreed knob): one stderr line
   // per launch with its epoch, grid, view key and completion sequence
   c->diag_trace = env_ll("MPIGX_DIAG_TRACE", 0) != 0;  // per rank: fault injection, not a knob

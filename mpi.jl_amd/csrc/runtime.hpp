@@ -251,9 +251,9 @@ struct mpigx_comm {
   int bcast_mode = 0;                   // MPIGX_BCAST: 0 auto, 1 direct, 2 sag
   int ring_channels = 1;                // MPIGX_RING_CHANNELS
   unsigned long long* stamps = nullptr; // diagnostic phase timestamps (mpigx_comm_set_stamps)
-  bool share_headroom = true;           // ranks sharing a device leave one block per CU free (kernel_cap)
-  bool scan_pp = false;                 // pull-push Scan / Exscan (kernels.hpp scan_pp_body)
-  bool shared_gate = true;              // ranks sharing a device meet on the host before launches (shared_gate)
+  bool share_headroom = false;          // MPIGX_SHARE_HEADROOM: ranks sharing a device leave one block per CU free
+  bool scan_pp = true;                  // MPIGX_SCAN_PP: pull-push Scan / Exscan (kernels.hpp scan_pp_body)
+  bool shared_gate = true;              // MPIGX_SHARED_GATE: ranks sharing a device meet on the host first
   bool diag_trace = false;              // MPIGX_DIAG_TRACE: one stderr line per launch (diagnostic)
   unsigned ll_gen = 0;                  // LL flag generation (epoch >> 31) the LL area was cleared for
   int test_import_fail = 0;             // MPIGX_TEST_IMPORT_FAIL: fail that many peer imports (tests)
