@@ -221,6 +221,12 @@ int mpigx_comm_set_timeout(mpigx_comm_t comm, long long ms);
  * it.  A peer whose mine[] entry on its side differs from my theirs[] entry
  * for it sees another memory than the one I write.  Local. */
 int mpigx_comm_diag_slots(mpigx_comm_t comm, int block, unsigned long long *mine, unsigned long long *theirs);
+/* Diagnostic, local, never waits on the device (callable from a watchdog
+ * thread): out[0] = my stream busy (0 idle, 1 busy, 2 error), [1] completion
+ * word, [2] the word awaited, [3] blocks counted so far, [4] launch sequence,
+ * [5] epoch, [6] my control-plane allgather sequence, [7] the lowest one any
+ * rank has posted. */
+int mpigx_comm_diag_state(mpigx_comm_t comm, unsigned long long *out);
 /* Diagnostic, COLLECTIVE: every rank writes `nonce` ^ rank into its own
  * signal arrays (through its own mapping), then reads every peer's through
  * its IPC mapping of it.  *stale = bitmask of the ranks whose array some rank

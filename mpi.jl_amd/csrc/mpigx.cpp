@@ -16,6 +16,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -256,7 +257,7 @@ namespace {
     }                                                                              \
   } while (0)
 
-int host_allgather(mpigx_comm* c, const void* mine, int len, void* out);
+int host_allgather_wait(mpigx_comm* c, const void* mine, int len, void* out, bool until_gone);
 
 // Ranks sharing a GPU (the test box; one rank per GPU never takes this):
 // before a collective kernel is enqueued, this rank's earlier work on the
@@ -265,13 +266,18 @@ int host_allgather(mpigx_comm* c, const void* mine, int len, void* out);
 // microseconds.  Without it, ranks that arrived early spin on the device that
 // the late rank's own kernels need: with 8 ranks on one GPU a late rank's
 // torch compare (nonzero) took 5.7 s and a device synchronize over a minute
-// while its peers spun (r04k), and calls timed out.  Blocking communicators
-// only (stream-ordered ones cannot wait); MPIGX_SHARED_GATE=0 disables it.
+// while its peers spun (r04k), and calls timed out.  The wait has no time
+// limit while the late rank's process lives: its own stream can stay busy
+// for over a minute with torch work alone when 8 processes share the GPU
+// (r04q: a rank's torch.nonzero kernels, no collective kernel of anyone
+// running), and a collective must not fail for a late peer.  Blocking
+// communicators only (stream-ordered ones cannot wait); MPIGX_SHARED_GATE=0
+// disables it.
 int shared_gate(mpigx_comm* c) {
   if (c->dev_share <= 1 || !c->blocking || !c->shared_gate || c->n == 1) return MPIGX_SUCCESS;
   HIPCK(hipStreamSynchronize(c->stream));
   int z = 0, all[kMaxRanks];
-  return host_allgather(c, &z, sizeof z, all);
+  return host_allgather_wait(c, &z, sizeof z, all, true);
 }
 
 PeerView make_view(mpigx_comm* c) {
@@ -1451,7 +1457,17 @@ int copy_n1(mpigx_comm* c, void* dst, const void* src, size_t bytes) {
 // Host control plane: allgather of <= 64-byte blobs through the shm block
 // (double-buffered by sequence parity: a rank can only reuse a buffer after
 // every peer posted the next sequence, i.e. finished reading it).
-int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
+// A peer process that no longer exists (a live one we may not signal still
+// counts as alive).
+bool peer_gone(const mpigx_comm* c, int q) {
+  const int pid = c->shm->ranks[q].pid;
+  return pid > 0 && kill(pid, 0) != 0 && errno == ESRCH;
+}
+
+// until_gone: wait for as long as the peer's process lives (MPI semantics: a
+// collective waits for a late rank) instead of failing after the
+// communicator's timeout; a note goes to stderr once that timeout has passed.
+int host_allgather_wait(mpigx_comm* c, const void* mine, int len, void* out, bool until_gone) {
   if (len > 256) return MPIGX_ERR_INTERN;
   if (c->n == 1 || !c->shm) {
     memcpy(out, mine, len);
@@ -1462,18 +1478,40 @@ int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
   memcpy(me.xbuf[k & 1], mine, len);
   me.xseq.store(k, std::memory_order_release);
   const double t0 = now_s(), limit = c->timeout_ticks / 1e8;
+  bool noted = false;
+  double next_check = t0 + 1.0;
   for (int q = 0; q < c->n; ++q) {
     unsigned spins = 0;
     while (c->shm->ranks[q].xseq.load(std::memory_order_acquire) < k) {
       if ((spins & 63) == 0) rt::progress_all(c);
-      if ((++spins & 4095) == 0 && now_s() - t0 > limit) {
-        c->broken = true;
-        return MPIGX_ERR_OTHER;
+      if ((++spins & 4095) == 0) {
+        const double t = now_s();
+        if (!until_gone && t - t0 > limit) {
+          c->broken = true;
+          return MPIGX_ERR_OTHER;
+        }
+        if (until_gone && t > next_check) {
+          next_check = t + 1.0;
+          if (peer_gone(c, q)) {
+            fprintf(stderr, "mpigx: rank %d: rank %d's process is gone\n", c->rank, q);
+            c->broken = true;
+            return MPIGX_ERR_OTHER;
+          }
+          if (!noted && t - t0 > limit) {
+            noted = true;
+            fprintf(stderr, "mpigx: rank %d has waited %.0f s for rank %d to reach the collective\n", c->rank,
+                    t - t0, q);
+          }
+          sched_yield();
+        }
       }
     }
     memcpy((char*)out + (size_t)q * len, c->shm->ranks[q].xbuf[k & 1], len);
   }
   return MPIGX_SUCCESS;
+}
+int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
+  return host_allgather_wait(c, mine, len, out, false);
 }
 
 // Per-rank description of a personalised exchange (see VArgs in common.hpp).
@@ -2379,6 +2417,28 @@ int mpigx_comm_diag_slots(mpigx_comm_t c, int block, unsigned long long* mine, u
       return MPIGX_ERR_INTERN;
     }
   }
+  return MPIGX_SUCCESS;
+}
+int mpigx_comm_diag_state(mpigx_comm_t c, unsigned long long* out) {
+  if (!c || !out) return MPIGX_ERR_COMM;
+  // no call here waits on the device: safe from a watchdog thread while the
+  // owner is blocked in a synchronize
+  const hipError_t q = hipStreamQuery(c->stream);
+  (void)hipGetLastError();
+  out[0] = q == hipSuccess ? 0 : (q == hipErrorNotReady ? 1 : 2);
+  out[1] = c->done ? *c->done : 0;
+  out[2] = c->done_target;
+  out[3] = c->dcount_total;
+  out[4] = c->launch_seq;
+  out[5] = c->epoch;
+  out[6] = c->xseq;
+  unsigned long long mn = ~0ull;
+  if (c->shm)
+    for (int q2 = 0; q2 < c->n; ++q2) {
+      const unsigned long long s = c->shm->ranks[q2].xseq.load(std::memory_order_acquire);
+      mn = s < mn ? s : mn;
+    }
+  out[7] = c->shm ? mn : 0;
   return MPIGX_SUCCESS;
 }
 int mpigx_comm_diag_mapcheck(mpigx_comm_t c, unsigned long long nonce, unsigned* stale) {

@@ -53,6 +53,7 @@ PROTOTYPES = {
     "mpigx_comm_release": (c_int, [c_void_p]),
     "mpigx_comm_diag_slots": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     "mpigx_comm_diag_mapcheck": (c_int, [c_void_p, ctypes.c_ulonglong, c_void_p]),
+    "mpigx_comm_diag_state": (c_int, [c_void_p, c_void_p]),
     "mpigx_comm_zc_stats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]),
     "mpigx_comm_host_stats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "mpigx_comm_ar_choice": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double),
