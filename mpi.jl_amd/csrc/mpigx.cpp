@@ -275,7 +275,14 @@ int host_allgather_wait(mpigx_comm* c, const void* mine, int len, void* out, boo
 // disables it.
 int shared_gate(mpigx_comm* c) {
   if (c->dev_share <= 1 || !c->blocking || !c->shared_gate || c->n == 1) return MPIGX_SUCCESS;
-  HIPCK(hipStreamSynchronize(c->stream));
+  // poll first: a drained (or nearly drained) stream is the common case in a
+  // loop of collectives, and the query costs far less than a synchronize
+  const double t0 = now_s();
+  hipError_t q;
+  while ((q = hipStreamQuery(c->stream)) == hipErrorNotReady && now_s() - t0 < 2e-3) {
+  }
+  if (q == hipErrorNotReady) HIPCK(hipStreamSynchronize(c->stream));
+  else if (q != hipSuccess) HIPCK(q);
   int z = 0, all[kMaxRanks];
   return host_allgather_wait(c, &z, sizeof z, all, true);
 }
