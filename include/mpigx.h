@@ -174,8 +174,9 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
                                          block handed out dynamically (0, default: one static slice per
                                          block; 1-64) */
 #define MPIGX_KNOB_SCAN_PP 16        /* MPIGX_SCAN_PP: 0/1, pull-push Scan / Exscan at n <= 8 (default 1) */
-#define MPIGX_KNOB_SHARE_HEADROOM 17 /* MPIGX_SHARE_HEADROOM: 0/1, ranks sharing a GPU leave one block per CU
-                                        free in the spinning kernels' grid caps (default 0) */
+#define MPIGX_KNOB_SHARE_HEADROOM 17 /* MPIGX_SHARE_HEADROOM: -1/0/1, ranks sharing a GPU leave one block per
+                                        CU free in the spinning kernels' grid caps (default -1: when 4 or
+                                        more ranks share it) */
 #define MPIGX_KNOB_SHARED_GATE 18    /* MPIGX_SHARED_GATE: 0/1, ranks sharing a GPU drain their stream and meet
                                         on the host before each collective launch (default 1) */
 #define MPIGX_KNOB_COUNT 19

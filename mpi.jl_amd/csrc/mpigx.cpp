@@ -431,7 +431,11 @@ int finish(mpigx_comm* c) {
 int kernel_cap(mpigx_comm* c, int occ) {
   const long long share = c->dev_share > 0 ? c->dev_share : 1;
   long long cap;
-  if (share > 1 && c->share_headroom)
+  // headroom: auto (< 0) = 4 or more ranks on the device (r04u: at 8 ranks
+  // one rank's scan blocks became resident only when the others' blocks gave
+  // up 30 s later — grids that exactly fill every CU slot leave no slack)
+  const bool headroom = c->share_headroom > 0 || (c->share_headroom < 0 && share >= 4);
+  if (share > 1 && headroom)
     cap = occ >= 2 ? (long long)c->cus_min * (occ - 1) / share : (long long)c->cus_min * 3 / (4 * share);
   else if (share > 1)
     cap = (long long)c->cus_min * (occ >= 6 ? occ - 1 : occ > 0 ? occ : 1) / share;
@@ -1746,7 +1750,7 @@ long long knob_value(const mpigx_comm* c, int k) {
     case MPIGX_KNOB_LL_MAX: return c->ll_max;
     case MPIGX_KNOB_AR_SLICES: return c->ar_slices;
     case MPIGX_KNOB_SCAN_PP: return c->scan_pp ? 1 : 0;
-    case MPIGX_KNOB_SHARE_HEADROOM: return c->share_headroom ? 1 : 0;
+    case MPIGX_KNOB_SHARE_HEADROOM: return c->share_headroom;
     case MPIGX_KNOB_SHARED_GATE: return c->shared_gate ? 1 : 0;
     default: return -1;
   }
@@ -1831,8 +1835,8 @@ int knob_apply(mpigx_comm* c, int k, long long v, bool init) {
       c->scan_pp = v != 0;
       return MPIGX_SUCCESS;
     case MPIGX_KNOB_SHARE_HEADROOM:
-      if (!in(0, 1)) return MPIGX_ERR_ARG;
-      c->share_headroom = v != 0;
+      if (!in(-1, 1)) return MPIGX_ERR_ARG;
+      c->share_headroom = (int)v;
       return MPIGX_SUCCESS;
     case MPIGX_KNOB_SHARED_GATE:
       if (!in(0, 1)) return MPIGX_ERR_ARG;
@@ -1905,10 +1909,15 @@ int knobs_from_env(mpigx_comm* c) {
   // not recur with the kernel's checked preconditions: the GPU suite with it
   // forced and the 8-rank headline / sequence / large-count cases, r04n)
   c->scan_pp = env_ll("MPIGX_SCAN_PP", 1) != 0;
-  // no residency headroom since round 4: the n = 8 cases pass without it and
-  // the same-device pull-push kernel takes 270 us at 256 blocks against 285
-  // at 128 (r04n coll_prof); MPIGX_SHARE_HEADROOM=1 restores it
-  c->share_headroom = env_ll("MPIGX_SHARE_HEADROOM", 0) != 0;
+  // residency headroom (-1 = auto: on when 4 or more ranks share the GPU;
+  // 0 off, 1 on for any sharing).  Off at 2 ranks: the same-device pull-push
+  // kernel takes 270 us at 256 blocks against 285 at 128 (r04n coll_prof)
+  // and no 2-rank run ever left a block unscheduled; on at 8, where r04u
+  // recorded one (kernel_cap)
+  {
+    const long long h = env_ll("MPIGX_SHARE_HEADROOM", -1);
+    c->share_headroom = h < 0 ? -1 : h > 0 ? 1 : 0;
+  }
   c->shared_gate = env_ll("MPIGX_SHARED_GATE", 1) != 0;
   return MPIGX_SUCCESS;
 }

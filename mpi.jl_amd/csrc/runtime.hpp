@@ -251,7 +251,7 @@ struct mpigx_comm {
   int bcast_mode = 0;                   // MPIGX_BCAST: 0 auto, 1 direct, 2 sag
   int ring_channels = 1;                // MPIGX_RING_CHANNELS
   unsigned long long* stamps = nullptr; // diagnostic phase timestamps (mpigx_comm_set_stamps)
-  bool share_headroom = false;          // MPIGX_SHARE_HEADROOM: ranks sharing a device leave one block per CU free
+  int share_headroom = -1;              // MPIGX_SHARE_HEADROOM: ranks sharing a device leave one block per CU free (-1 auto: >= 4 ranks)
   bool scan_pp = true;                  // MPIGX_SCAN_PP: pull-push Scan / Exscan (kernels.hpp scan_pp_body)
   bool shared_gate = true;              // MPIGX_SHARED_GATE: ranks sharing a device meet on the host first
   bool diag_trace = false;              // MPIGX_DIAG_TRACE: one stderr line per launch (diagnostic)
