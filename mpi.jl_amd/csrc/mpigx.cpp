@@ -1468,11 +1468,22 @@ int copy_n1(mpigx_comm* c, void* dst, const void* src, size_t bytes) {
 // Host control plane: allgather of <= 64-byte blobs through the shm block
 // (double-buffered by sequence parity: a rank can only reuse a buffer after
 // every peer posted the next sequence, i.e. finished reading it).
-// A peer process that no longer exists (a live one we may not signal still
-// counts as alive).
+// A peer process that no longer runs: gone, or exited and not yet reaped by
+// its parent (a zombie still answers kill(pid, 0)).  A live one we may not
+// signal counts as alive.
 bool peer_gone(const mpigx_comm* c, int q) {
   const int pid = c->shm->ranks[q].pid;
-  return pid > 0 && kill(pid, 0) != 0 && errno == ESRCH;
+  if (pid <= 0) return false;
+  if (kill(pid, 0) != 0) return errno == ESRCH;
+  char path[64], buf[256];
+  snprintf(path, sizeof path, "/proc/%d/stat", pid);
+  FILE* f = fopen(path, "r");
+  if (!f) return false;
+  const size_t len = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[len] = 0;
+  const char* e = strrchr(buf, ')');  // "pid (comm) S ..."
+  return e && e[1] == ' ' && (e[2] == 'Z' || e[2] == 'X');
 }
 
 // until_gone: wait for as long as the peer's process lives (MPI semantics: a
