@@ -1524,8 +1524,10 @@ int host_allgather_wait(mpigx_comm* c, const void* mine, int len, void* out, boo
             fprintf(stderr, "mpigx: rank %d has waited %.0f s for rank %d to reach the collective\n", c->rank,
                     t - t0, q);
           }
-          sched_yield();
         }
+        // a long wait: leave the host cores to the late rank (with several
+        // ranks per GPU the waiters would otherwise spin on every core)
+        if (until_gone && t - t0 > 0.05) usleep(200);
       }
     }
     memcpy((char*)out + (size_t)q * len, c->shm->ranks[q].xbuf[k & 1], len);
