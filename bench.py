@@ -173,6 +173,30 @@ def bench_local(args):
     def step():
         MPI.reduce_local_multi(ins, out, MPI.SUM, stream=stream)
 
+    # the box's own ceiling for this kernel: a read-only
+    # stream of the same 8 inputs in the fold's access layout, no fold, no
+    # stores (mpigx_read_probe, copy.hip read_probe_kernel), HIP-event timed on
+    # the same stream; MI355X boxes differ in HBM read rate by ~8 %
+    # (profiles/r02_fold_tune_box*.json), so roofline.frac_vs_measured is the
+    # number that is comparable from box to box
+    import ctypes
+    sink = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    in_ptrs = (ctypes.c_void_p * len(ins))(*[x.data_ptr() for x in ins])
+
+    def read_probe_ms(reps=10):
+        L = MPI.lib()
+        for _ in range(2):
+            MPI.api._check(L.mpigx_read_probe(in_ptrs, len(ins), S, ctypes.c_void_p(sink.data_ptr()),
+                                              ctypes.c_void_p(stream.cuda_stream)))
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            L.mpigx_read_probe(in_ptrs, len(ins), S, ctypes.c_void_p(sink.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
+
+    read_ms = [read_probe_ms()] if len(ins) in (1, 2, 4, 8) else []
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -189,6 +213,10 @@ def bench_local(args):
     wall = (time.perf_counter() - t0) / args.steps
     kern_ms = e0.elapsed_time(e1) / args.steps
     algo = (args.nbuf + 1) * S
+    if read_ms:
+        read_ms.append(read_probe_ms())
+    # the box's read rate: the faster of the two probes (before / after the timed steps)
+    peak_measured = (args.nbuf * S) / (min(read_ms) / 1e3) / 1e9 if read_ms else None
 
     # parity spot check of the timed output vs the MPICH-pinned oracle (1 Mi elements)
     import numpy as np
@@ -253,6 +281,11 @@ def bench_local(args):
                    "algorithmic_bytes_per_step": algo},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "peak_measured": round(peak_measured, 1) if peak_measured else None,
+                     "frac_vs_measured": round(achieved / peak_measured, 4) if peak_measured else None,
+                     "peak_measured_basis": "this box's read-only stream of the same 8 inputs in the fold's access "
+                                            "layout (mpigx_read_probe: 8 x 256 MiB read, nothing written), HIP events, "
+                                            "faster of one probe before and one after the timed steps",
                      "kernel": "fold_local_kernel<OpSum,float,NMAX 8,TREE,SH_FULL,U 4>", "kernel_ms": round(kern_ms, 4),
                      "achieved_basis": "9 x 256 MiB algorithmic bytes / (HIP-event time over the K timed launches on the launch stream / K)",
                      "traffic_basis": "rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE per dispatch (gfx950 FETCH_SIZE "

@@ -175,11 +175,15 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
                                          block; 1-64) */
 #define MPIGX_KNOB_SCAN_PP 16        /* MPIGX_SCAN_PP: 0/1, pull-push Scan / Exscan at n <= 8 (default 1) */
 #define MPIGX_KNOB_SHARE_HEADROOM 17 /* MPIGX_SHARE_HEADROOM: -1/0/1, ranks sharing a GPU leave one block per
-                                        CU free in the spinning kernels' grid caps (default -1: when 4 or
-                                        more ranks share it) */
+                                        CU free in the spinning kernels' grid caps (default -1 = 1: whenever
+                                        ranks share it; 0 only for measurements) */
 #define MPIGX_KNOB_SHARED_GATE 18    /* MPIGX_SHARED_GATE: 0/1, ranks sharing a GPU drain their stream and meet
                                         on the host before each collective launch (default 1) */
-#define MPIGX_KNOB_COUNT 19
+#define MPIGX_KNOB_PEER_MEM 19       /* MPIGX_PEER_MEM: 0 "auto" (default), 1 "xdev": every peer is treated as
+                                        on another GPU (uncached signal arrays and LL areas, the
+                                        one-rank-per-GPU protocol) even when it shares this one; a test
+                                        knob that runs the production signalling on a 1-GPU box (init only) */
+#define MPIGX_KNOB_COUNT 20
 #define MPIGX_ALGO_AUTO 0     /* unset: static rules + the measured choices */
 #define MPIGX_ALGO_LL 1       /* "ll" */
 #define MPIGX_ALGO_LL2 2      /* "ll2" */
@@ -206,66 +210,13 @@ int mpigx_comm_get_knob(mpigx_comm_t comm, int knob, long long *value);
  * cap is *cap x its resident blocks per CU). */
 int mpigx_comm_device_share(mpigx_comm_t comm, int *ranks, int *cap);
 
-/* Diagnostic: per-block phase timestamps of the collective kernels (100 MHz
- * device wall clock).  stamps = device buffer of >= 1024 x 8 u64 (NULL
- * disables); slot [block][k]: 0 entry, 1 after the entry barrier, 2 after the
- * reduce-scatter, 3 after the middle barrier, 4 after the allgather, 5 after
- * the exit barrier.  Local (not collective). */
-int mpigx_comm_set_stamps(mpigx_comm_t comm, void *stamps);
 /* How long a collective's blocks wait for a peer before the call fails with
  * MPI_ERR_OTHER and the communicator is marked broken (default
  * MPIGX_TIMEOUT_MS, 60000).  Local; applies to later calls.  ms >= 1. */
 int mpigx_comm_set_timeout(mpigx_comm_t comm, long long ms);
-/* Diagnostic: barrier slot row `block` as this rank sees it.  mine[q] = the
- * word peer q last stored into MY signal array (my own mapping); theirs[q] =
- * the word I last stored into peer q's array, read back through MY mapping of
- * it.  A peer whose mine[] entry on its side differs from my theirs[] entry
- * for it sees another memory than the one I write.  Local. */
-int mpigx_comm_diag_slots(mpigx_comm_t comm, int block, unsigned long long *mine, unsigned long long *theirs);
-/* Diagnostic, local, never waits on the device (callable from a watchdog
- * thread): out[0] = my stream busy (0 idle, 1 busy, 2 error), [1] completion
- * word, [2] the word awaited, [3] blocks counted so far, [4] launch sequence,
- * [5] epoch, [6] my control-plane allgather sequence, [7] the lowest one any
- * rank has posted. */
-int mpigx_comm_diag_state(mpigx_comm_t comm, unsigned long long *out);
-/* Diagnostic, COLLECTIVE: every rank writes `nonce` ^ rank into its own
- * signal arrays (through its own mapping), then reads every peer's through
- * its IPC mapping of it.  *stale = bitmask of the ranks whose array some rank
- * (any) saw without the new nonce: that peer's mapping and the owner's no
- * longer alias one memory.  Every rank gets the same mask. */
-int mpigx_comm_diag_mapcheck(mpigx_comm_t comm, unsigned long long nonce, unsigned *stale);
-/* Zero-copy paths (user buffers mapped by the peers over IPC): how many
- * launches ran on a cached view without any host exchange, and how many
- * host exchanges of buffer registrations there were.  Diagnostic. */
-int mpigx_comm_zc_stats(mpigx_comm_t comm, unsigned long long *optimistic_hits,
-                        unsigned long long *exchanges);
-/* Host time of the last collective call from its entry to its first kernel
- * launch (argument checks, planning, zero-copy view resolution).  Diagnostic. */
-int mpigx_comm_host_stats(mpigx_comm_t comm, double *prelaunch_us);
-/* Large (zero-copy-sized) Allreduce algorithm the communicator measured and
- * chose (MPIGX_AR_TUNE): *choice = -1 undecided, 0 pull two-shot, 1 push
- * two-shot, 2 pull-push two-shot (MPIGX_ALGO_PULLPUSH); *pull_ns_per_mib /
- * *push_ns_per_mib = this rank's measured device time per MiB of message
- * (0 = not measured).  Diagnostic. */
-int mpigx_comm_ar_choice(mpigx_comm_t comm, int *choice, double *pull_ns_per_mib, double *push_ns_per_mib);
-/* The same with every candidate's cost: ns_per_mib[0..2] = pull, push,
- * pull-push (this rank's device ns per MiB; 0 = not measured).  Diagnostic. */
-int mpigx_comm_ar_costs(mpigx_comm_t comm, int *choice, double *ns_per_mib);
-/* Smaller collectives (below the zero-copy size), size class
- * log2_bytes = floor(log2(message bytes)) + 64 * kind (kind 0 Allreduce,
- * 1 Bcast, 2 Allgather, 3 Alltoall; the byte movers' class is the per-rank
- * block): the algorithm the communicator measured and chose (*choice = -1
- * undecided / not tuned, 0 LL step, 1 staged one-shot (byte movers: the
- * staged copy), 2 staged two-shot, 3 LL two-shot) and this rank's best device
- * time per MiB of each (ns_per_mib[4], 0 = not a candidate or not measured).
- * Diagnostic. */
-int mpigx_comm_tune_class(mpigx_comm_t comm, int log2_bytes, int *choice, double *ns_per_mib);
 
-/* Diagnostic (bench roofline denominator): every rank pulls `bytes` from
- * every peer's staging arena at once (kind 0: aggregate xGMI ingress) or
- * from rank+1 only (kind 1: one link).  *seconds = device time of the pull
- * (includes one cross-rank barrier).  Collective. */
-int mpigx_comm_probe(mpigx_comm_t comm, int kind, long long bytes, double *seconds);
+/* Diagnostics (phase stamps, signal-slot and mapping checks, tuner and
+ * zero-copy statistics, fabric probes): include/mpigx_diag.h. */
 
 /* ---- collectives (src/collective.jl ccall sites) ------------------------- */
 /* MPI_Barrier  — collective.jl:15-19 */

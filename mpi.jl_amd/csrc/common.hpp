@@ -158,7 +158,37 @@ struct PeerView {
   uint64_t* sig_uc;            // my uncached signal array (cross-device writers)
   uint64_t* sig_rw;            // my cached signal array (same-device writers and myself)
   const char* ll_rw;           // my cached LL area at this launch's parity (same-device senders)
+  // Waiting for a late peer (round 5, DESIGN §3 "a late rank"): a blocking
+  // call's host watches its peers while it waits (mpigx.cpp finish), so its
+  // kernel's polls never give up on time alone — they give up when the host
+  // stores a nonzero `cancel` word (a peer's process is gone, its
+  // communicator failed, or every rank's kernel has been stuck past the
+  // timeout).  Stream-ordered launches (nobody watching: cancel = null) keep
+  // the timeout.  Block 0 stores `kseq` (this launch's number, the same on
+  // every rank) into `started` at entry, which tells the host — and through
+  // the shm block its peers — which launch its GPU is in.
+  unsigned long long kseq;
+  unsigned long long* started;
+  const unsigned* cancel;
+  // Integrity of the argument block (zero-copy launches, device.hpp
+  // zc_enter): a checksum over the block's first args_words 32-bit words (this
+  // PeerView is its first member; the args_sum word itself counted as 0),
+  // checked before any pointer in it is used.  0 words = unchecked.
+  unsigned args_words;
+  unsigned args_sum;
 };
+// Checksum of an argument block (host and device; mpigx.cpp seal_args,
+// device.hpp args_intact): word i mixed with its index, summed — a permuted,
+// stale or partly overwritten block does not match.
+__host__ __device__ inline unsigned args_mix(unsigned w, unsigned i) {
+  unsigned x = w ^ (i * 0x9E3779B9u);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
 // the array peer `from` writes its words for me into
 __host__ __device__ inline uint64_t* sig_in(const PeerView& pv, int from) {
   return ((pv.rw_mask >> from) & 1u) ? pv.sig_rw : pv.sig_uc;
@@ -203,6 +233,10 @@ struct FoldArgs {
   unsigned ll_flag;    // this launch's flag (never 0, never a stale flag of the same parity)
   int dyn;             // ar_zc_kernel AG_PUSH: 1 = slices of `slice` elements handed out by a ticket counter
   int own;             // M_RED_ZC (ar_zc_kernel): index of the chunk this rank folds (root: none at n >= 3)
+  // ar_zc_kernel AG_PUSH: bytes of rank q's allocation from zc_recv[q] to its
+  // end (the agreed view's exported sizes): the remote stores are checked
+  // against them before any is made
+  long long zc_avail[kMaxRanks];
 };
 
 // Ring reduce-scatter + allgather (MPIGX_ALGO=ring; kernels.hpp ring_kernel).
@@ -329,6 +363,10 @@ struct ScanArgs {
   int pp;              // 1: pull-push zero-copy (n <= 8): rank r computes EVERY rank's result for chunk r
   long long chunk;     // pp: elements per rank chunk (multiple of vec)
   char* zrecv[kMaxRanks];  // pp: every rank's recvbuf (zero-copy view)
+  // pp: bytes of rank q's allocation from src[q] / zrecv[q] to its end (the
+  // agreed view's exported sizes), checked before any load or store
+  long long zs_avail[kMaxRanks];
+  long long zr_avail[kMaxRanks];
 };
 
 }  // namespace mpigx

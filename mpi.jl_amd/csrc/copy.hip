@@ -23,6 +23,7 @@ __global__ __launch_bounds__(kThreads) void copy_kernel(CopyArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(CopyArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
+  kernel_started(sA.pv);
   stamp(sA.pv, 0);
   const int ab = copy_body<NMAX, U>(sA);
   signal_done(sA.pv, ab);
@@ -150,11 +151,11 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
       if (!bc || p == A.root) {
         char* dst = bc ? recv : recv + (long long)p * A.total;
         for (long long i = l0 + tid; i < l1 && ok; i += nt) {
-          ok = ll_get(in, i, flag, t0, pv.timeout_ticks, &d);
+          ok = ll_get(pv, in, i, flag, t0, &d);
           if (ok) ll_store8(dst, i, A.bytes, d);
         }
       } else if (b == 0 && tid == 0) {
-        ok = ll_get(in, 0, flag, t0, pv.timeout_ticks, &d);
+        ok = ll_get(pv, in, 0, flag, t0, &d);
       }
     }
     if (!ok) __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -423,6 +424,7 @@ __device__ __forceinline__ void vx_body(const VArgs& A) {
 
 template <int NMAX, int U>
 __global__ __launch_bounds__(kThreads) void vx_kernel(VArgs A) {
+  kernel_started(A.pv);
   vx_body<NMAX, U>(A);
   signal_done(A.pv);
 }
@@ -509,6 +511,61 @@ hipError_t launch_copy(dim3 grid, hipStream_t s, const CopyArgs& a) {
   else if (n <= 4) hipLaunchKernelGGL((copy_kernel<4, 4>), grid, dim3(kThreads), 0, s, a);
   else if (n <= 8) hipLaunchKernelGGL((copy_kernel<8, 2>), grid, dim3(kThreads), 0, s, a);
   else hipLaunchKernelGGL((copy_kernel<16, 1>), grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Read-only stream of nin HBM buffers (mpigx_diag.h mpigx_read_probe): the
+// ceiling of config 2's fold on the box it runs on.  Same access layout as
+// fold_local_kernel<SH_FULL, U = 4> (thread t of block b reads the four
+// 16-B vectors (4b+u)*256 + t of every input, all nin x 4 non-temporal loads
+// in flight before any use) with the fold and the store removed: the loads
+// are XOR-ed into a register that is stored only if it equals a value it
+// never takes, so the compiler keeps every load and the kernel writes nothing.
+// ---------------------------------------------------------------------------
+struct ReadProbeArgs {
+  const char* in[kMaxRanks];
+  int nin;
+  long long nvec;  // 16-B vectors per input
+  u32x4* sink;
+};
+template <int NIN>
+__global__ __launch_bounds__(kThreads) void read_probe_kernel(ReadProbeArgs A) {
+  constexpr int U = 4;
+  u32x4 acc = {0, 0, 0, 0};
+  const long long step = (long long)gridDim.x * (U * kThreads);
+  for (long long v0 = (long long)blockIdx.x * (U * kThreads) + threadIdx.x; v0 < A.nvec; v0 += step) {
+    u32x4 x[U][NIN];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s = 0; s < NIN; ++s) {
+        const long long k = v0 + (long long)u * kThreads;
+        x[u][s] = ld16(A.in[s] + 16 * (k < A.nvec ? k : A.nvec - 1));
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s = 0; s < NIN; ++s) acc ^= x[u][s];
+  }
+  if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u && acc.z == 0x85ebca6bu) A.sink[threadIdx.x] = acc;
+}
+
+hipError_t launch_read_probe(const void* const* in, int nin, long long bytes, void* sink, hipStream_t s) {
+  ReadProbeArgs a;
+  for (int k = 0; k < kMaxRanks; ++k) a.in[k] = k < nin ? (const char*)in[k] : nullptr;
+  a.nin = nin;
+  a.nvec = bytes / 16;
+  a.sink = (u32x4*)sink;
+  const long long g = (a.nvec + 4 * kThreads - 1) / (4 * kThreads);
+  const dim3 grid((unsigned)(g < 1 ? 1 : g > (1ll << 30) ? (1ll << 30) : g));
+  switch (nin) {
+    case 1: hipLaunchKernelGGL(read_probe_kernel<1>, grid, dim3(kThreads), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(read_probe_kernel<2>, grid, dim3(kThreads), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(read_probe_kernel<4>, grid, dim3(kThreads), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(read_probe_kernel<8>, grid, dim3(kThreads), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -903,6 +903,30 @@ __device__ __forceinline__ void spin_pause(unsigned& k) {
   ++k;
 }
 
+// When a poll loop gives up (PeerView.cancel): a stream-ordered launch after
+// timeout_ticks; a blocking one only when its host stores the cancel word
+// (read once per kCancelPoll of waiting — a PCIe read of a host-pinned word —
+// so a late peer is waited for as long as its host says it is coming).  A
+// zero timeout (a failed host gate) gives up at once either way.
+constexpr uint64_t kCancelPoll = 100000;  // 1 ms of the 100 MHz wall clock
+__device__ __forceinline__ bool spin_expired(const PeerView& pv, uint64_t t0, uint64_t& next) {
+  const uint64_t el = wall_clock64() - t0;
+  if (!pv.cancel || pv.timeout_ticks == 0) return el > pv.timeout_ticks;
+  if (el < next) return false;
+  next = el + kCancelPoll;
+  return __hip_atomic_load(pv.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
+// Kernel entry of every collective kernel: block 0 tells the host which
+// launch its GPU has reached (PeerView.started, one posted PCIe write), then
+// the phase stamp.
+__device__ __forceinline__ void kernel_started(const PeerView& pv) {
+  if (pv.started && blockIdx.x == 0 && threadIdx.x == 0) {
+    __hip_atomic_store(pv.started, pv.kseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+}
+
 // Phase timestamp k of this block (mpigx_comm_set_stamps, diagnostic): one
 // lane stores the 100 MHz device wall clock; a scalar branch when off.
 __device__ __forceinline__ void stamp(const PeerView& pv, int k) {
@@ -944,11 +968,11 @@ __device__ __forceinline__ bool rank_barrier(const PeerView& pv, uint64_t ep, in
       sig_put(peer_slot, word);
       uint64_t* mine = sig_in(pv, lane) + sig_index(blockIdx.x, lane);
       const uint64_t t0 = wall_clock64();
-      uint64_t v;
+      uint64_t v, next = kCancelPoll;
       unsigned k = 0;
       while (((v = sig_get(mine)) >> kSigShift) < ep) {
         spin_pause(k);
-        if (wall_clock64() - t0 > pv.timeout_ticks) {
+        if (spin_expired(pv, t0, next)) {
           ok = false;
           if (pv.stamps) {  // diagnostic: the epoch awaited and the word last seen from that peer
             pv.stamps[(size_t)blockIdx.x * 8 + 6] = ep;
@@ -1038,11 +1062,11 @@ __device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t e
       }
       const uint64_t* mine = sig_in(pv, lane) + sig_index(row, lane);
       const uint64_t t0 = wall_clock64();
-      uint64_t v;
+      uint64_t v, next = kCancelPoll;
       unsigned k = 0;
       while (((v = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> kSigShift) < ep) {
         spin_pause(k);
-        if (wall_clock64() - t0 > pv.timeout_ticks) {
+        if (spin_expired(pv, t0, next)) {
           ok = false;
           break;
         }
@@ -1069,7 +1093,58 @@ __device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t e
 // the host in the completion word itself (kernels.hpp signal_done): ONE store
 // carries both "done" and "aborted", so every rank's host reads the same
 // verdict — a separate flag word raced the completion store over PCIe.
+//
+// Before the barrier (round 5): the argument block must be
+// the one the host sealed for THIS launch — its checksum (args_intact) and,
+// for blocking launches, its completion base: at entry the device counter
+// holds every earlier launch's blocks and at most this launch's own, so a
+// stale block (an older launch's arguments) shows.  A zero-copy kernel
+// dereferences the peers' mapped buffers straight from this block; round 3
+// saw an aperture violation (an address past the legal range, not a missing
+// mapping) in the pull-push Scan on 5 of 8 ranks at once.  A block that fails
+// touches no pointer of it (the barrier's too): it records kErrProtocol and
+// leaves; its host breaks the communicator and says so in the shm block, and
+// every peer's host then cancels its own wait (mpigx.cpp finish), so all
+// ranks fail the call instead of one rank faulting the GPU.
+__device__ __noinline__ bool args_intact(const PeerView& pv, unsigned* why) {
+  __shared__ unsigned s_sum, s_ok;
+  if (threadIdx.x == 0) s_sum = 0;
+  __syncthreads();
+  const unsigned nw = pv.args_words;
+  if (nw) {
+    constexpr unsigned kSumWord = (unsigned)(offsetof(PeerView, args_sum) / 4);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&pv);
+    unsigned part = 0;
+    for (unsigned i = threadIdx.x; i < nw; i += blockDim.x) part += args_mix(i == kSumWord ? 0u : w[i], i);
+    atomicAdd(&s_sum, part);  // LDS atomic
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned ok = (nw == 0 || s_sum == pv.args_sum) ? 1u : 0u;
+    *why = ok ? 0u : 1u;
+    if (ok && pv.done) {
+      const unsigned long long c = __hip_atomic_load(pv.dcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (c < pv.dbase || c >= pv.dbase + gridDim.x) {
+        ok = 0u;
+        *why = 2u;
+      }
+    }
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
 __device__ __forceinline__ bool zc_enter(const PeerView& pv, uint64_t ep, int* abort, bool strict = true) {
+  unsigned why = 0;
+  if (!args_intact(pv, &why)) {
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(pv.err, kErrProtocol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (pv.stamps) pv.stamps[(size_t)blockIdx.x * 8 + 6] = 0xA765000000000000ull | why;
+    }
+    *abort = 1;
+    return false;
+  }
   *abort = pv.zc_bad;
   return rank_barrier(pv, ep, abort, pv.zc_key, true, true, strict);
 }
@@ -1090,11 +1165,13 @@ __device__ __forceinline__ void ll_put(char* area, long long i, uint64_t d, unsi
   __hip_atomic_store(q, (d & 0xffffffffull) | fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(q + 1, (d >> 32) | fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// waits for line i of a sender's area to carry `flag`; false on timeout
-__device__ __forceinline__ bool ll_get(const char* area, long long i, unsigned flag, uint64_t t0, uint64_t timeout,
+// waits for line i of a sender's area to carry `flag`; false when the wait
+// gives up (spin_expired; t0 = the start of the caller's wait)
+__device__ __forceinline__ bool ll_get(const PeerView& pv, const char* area, long long i, unsigned flag, uint64_t t0,
                                        uint64_t* d) {
   const uint64_t* q = reinterpret_cast<const uint64_t*>(area + kLLLine * i);
   unsigned k = 0;
+  uint64_t next = kCancelPoll;
   for (;;) {
     const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1102,7 +1179,7 @@ __device__ __forceinline__ bool ll_get(const char* area, long long i, unsigned f
       *d = (a & 0xffffffffull) | (b << 32);
       return true;
     }
-    if (wall_clock64() - t0 > timeout) return false;
+    if (spin_expired(pv, t0, next)) return false;
     spin_pause(k);
   }
 }
@@ -1133,7 +1210,7 @@ __device__ __forceinline__ void ll_store8(char* dst, long long i, long long byte
 // ---------------------------------------------------------------------------
 __device__ __noinline__ bool ll_exchange(const PeerView& pv, char* const* push, const char* in, long long stride,
                                          unsigned flag, const char* send, long long bytes, long long l0, long long l1,
-                                         char* unp, long long ustride, int n, int r, uint64_t timeout, unsigned* err) {
+                                         char* unp, long long ustride, int n, int r, unsigned* err) {
   __shared__ int s_ok;
   const long long tid = threadIdx.x, nt = blockDim.x;
   const bool al8 = (((uintptr_t)send) & 7) == 0;
@@ -1164,13 +1241,13 @@ __device__ __noinline__ bool ll_exchange(const PeerView& pv, char* const* push, 
     for (int p = 0; p < n && ok; ++p) {
       if (p == r) continue;
       const uint64_t* q = reinterpret_cast<const uint64_t*>(ll_from(pv, in, p, stride) + kLLLine * i);
-      uint64_t a, b;
+      uint64_t a, b, next = kCancelPoll;
       unsigned k = 0;
       for (;;) {
         a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((unsigned)(a >> 32) == flag && (unsigned)(b >> 32) == flag) break;
-        if (wall_clock64() - t0 > timeout) {
+        if (spin_expired(pv, t0, next)) {
           ok = false;
           break;
         }

@@ -80,6 +80,7 @@ __global__ __launch_bounds__(kThreads) void fold_kernel(FoldArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(FoldArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
+  kernel_started(sA.pv);
   stamp(sA.pv, 0);
   const int ab = fold_body<OP, T, NMAX, SCHED>(sA);
   signal_done(sA.pv, ab);
@@ -280,7 +281,13 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     char* dsts[NMAX];
     const char* srcs[NMAX];
     long long lens[NMAX];
-    stamp(pv, 0);
+    {  // phase 1 stores into the peers' arenas before any barrier (zc_enter's checks)
+      unsigned why = 0;
+      if (!args_intact(pv, &why)) {
+        if (tid == 0) __hip_atomic_store(pv.err, kErrProtocol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return 0;
+      }
+    }
     stamp(pv, 1);
     // phase 1: slice b of my chunk p -> rank p's slot [r], all peers at once
 #pragma unroll
@@ -346,7 +353,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     const long long bytes = A.count * es;
     const long long l0 = (lo * es) / 8, l1 = hi > lo ? (hi * es + 7) / 8 : l0;
     if (!ll_exchange(pv, A.zc_recv, A.ll_in, A.ll_stride, A.ll_flag, send, bytes, l0, l1, (char*)mine, A.slot_bytes,
-                     pv.n, pv.rank, pv.timeout_ticks, pv.err))
+                     pv.n, pv.rank, pv.err))
       return 0;
     if (A.mode == M_AR_LL || pv.rank == A.root)
       fold_range<OP, T, NMAX, SCHED, SH_PRE, FU>(A, src, src2, lo, hi, recv, nullptr, recv_vec, tid, nt);
@@ -390,7 +397,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       if (p == r) continue;
       for (long long i = rl0 + tid; i < rl1 && ok; i += nt) {
         uint64_t d;
-        ok = ll_get(ll_from(pv, A.ll_in, p, A.ll_stride), i, flag, t0, pv.timeout_ticks, &d);
+        ok = ll_get(pv, ll_from(pv, A.ll_in, p, A.ll_stride), i, flag, t0, &d);
         if (ok) *reinterpret_cast<uint64_t*>((char*)mine + (long long)p * A.slot_bytes + 8 * i) = d;
       }
     }
@@ -421,7 +428,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       span(p, &c0, &cb, &l0, &l1);
       for (long long i = l0 + tid; i < l1 && ok; i += nt) {
         uint64_t d;
-        ok = ll_get(ll_from(pv, A.ll_in, p, A.ll_stride) + half, i, flag, t0, pv.timeout_ticks, &d);
+        ok = ll_get(pv, ll_from(pv, A.ll_in, p, A.ll_stride) + half, i, flag, t0, &d);
         if (ok) ll_store8((char*)recv + c0 * es, i, cb, d);
       }
     }
@@ -529,6 +536,7 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
   const long long tid = threadIdx.x, nt = blockDim.x;
   uint64_t ep = pv.epoch;
   int ab;
+  kernel_started(pv);
   stamp(pv, 0);
   if (!zc_enter(pv, ep++, &ab)) {
     signal_done(pv, 0);
@@ -554,11 +562,20 @@ __global__ __launch_bounds__(kThreads) void ar_zc_kernel(FoldArgs A0) {
     const bool red = A.mode == M_RED_ZC;
     const int m = red ? 1 : n;
     T* outs[NMAX];
+    bool fits = true;  // my chunk's end inside every recvbuf I store into (the view's exported sizes)
 #pragma unroll
     for (int j = 0; j < NMAX; ++j) {
+      const int q = red ? A.root : (r + j) % n;
       outs[j] = red ? (T*)A.zc_recv[A.root] : recv;
-      if (!red && j > 0 && j < n) outs[j] = (T*)A.zc_recv[(r + j) % n];
-      if (j < m) vec &= ((uintptr_t)outs[j] & 15) == 0;
+      if (!red && j > 0 && j < n) outs[j] = (T*)A.zc_recv[q];
+      if (j < m) {
+        vec &= ((uintptr_t)outs[j] & 15) == 0;
+        fits &= outs[j] != nullptr && c1 * es <= A.zc_avail[q];
+      }
+    }
+    if (!ab && !fits) {  // the same verdict in every block: the exit barrier's abort bit reaches every peer block
+      ab = 1;
+      if (tid == 0) __hip_atomic_store(pv.err, kErrProtocol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (A.dyn) {
       // slices of my chunk handed out by a ticket counter (a block that
@@ -673,11 +690,12 @@ __device__ __forceinline__ bool ring_wait(const PeerView& pv, int from, uint64_t
   if (threadIdx.x == 0) {
     const uint64_t* slot = sig_in(pv, from) + sig_index(blockIdx.x, from);
     const uint64_t t0 = wall_clock64();
+    uint64_t next = kCancelPoll;
     int ok = 1;
     unsigned k = 0;
     while ((__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> kSigShift) < ep) {
       spin_pause(k);
-      if (wall_clock64() - t0 > pv.timeout_ticks) {
+      if (spin_expired(pv, t0, next)) {
         ok = 0;
         __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -770,6 +788,7 @@ __global__ __launch_bounds__(kThreads) void ring_kernel(RingArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(RingArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
+  kernel_started(sA.pv);
   const int ab = ring_body<OP, T>(sA);
   signal_done(sA.pv, ab);
 }
@@ -959,13 +978,23 @@ __device__ __forceinline__ int scan_pp_body(const ScanArgs& A) {
   if (!ab) {
     const long long c0 = lmin((long long)r * A.chunk, A.count), c1 = lmin(c0 + A.chunk, A.count);
     const long long lo = lmin(c0 + (long long)b * A.slice, c1), hi = lmin(lo + A.slice, c1);
-    // preconditions of every access below, checked instead of trusted: a
-    // violation stores nothing and fails the call (MPI_ERR_INTERN) instead of
-    // faulting the GPU (round 3 saw an aperture violation in this kernel)
+    // preconditions of every access below, checked instead of trusted (round
+    // 3 saw an aperture violation in this kernel): the partition, non-null
+    // operands, and the extents — my chunk's end inside every contribution I
+    // load and every recvbuf I store into, against the sizes of the
+    // allocations the peers exported for this view.  The verdict depends on
+    // the chunk, not the block, so every block of this rank reaches it; a
+    // violation stores nothing, fails the call here (MPI_ERR_INTERN) and sets
+    // the abort bit of the exit barrier, which every block of every peer
+    // receives — no rank completes with a chunk of its recvbuf unwritten.
+    const int nl = A.exclusive ? pv.n - 1 : pv.n;
+    const long long end = c1 * A.esize;
     bool sane = pv.n >= 2 && pv.n <= 8 && r < pv.n && 0 <= c0 && c0 <= lo && lo <= hi && hi <= c1 &&
                 c1 <= A.count;
-    for (int q = 0; q < pv.n; ++q) sane &= A.src[q] != nullptr && A.zrecv[q] != nullptr;
+    for (int q = 0; q < pv.n; ++q)
+      sane &= A.src[q] != nullptr && A.zrecv[q] != nullptr && end <= A.zr_avail[q] && (q >= nl || end <= A.zs_avail[q]);
     if (!sane) {
+      ab = 1;
       if (threadIdx.x == 0) {
         __hip_atomic_store(pv.err, kErrProtocol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (pv.stamps) pv.stamps[(size_t)b * 8 + 6] = 0xBAD0000000000000ull | (uint64_t)(hi - lo);
@@ -994,6 +1023,7 @@ __global__ __launch_bounds__(kThreads) void scan_kernel(ScanArgs A) {
   uint32_t* d = reinterpret_cast<uint32_t*>(&sA);
   for (unsigned i = threadIdx.x; i < sizeof(ScanArgs) / 4; i += blockDim.x) d[i] = w[i];
   __syncthreads();
+  kernel_started(sA.pv);
   stamp(sA.pv, 0);
   const int ab = sA.pp ? scan_pp_body<OP, T>(sA) : scan_body<OP, T>(sA);
   signal_done(sA.pv, ab);
@@ -1014,7 +1044,7 @@ __device__ __forceinline__ int scan_body(const ScanArgs& A) {  // returns the ab
     const long long es = A.esize, bytes = A.count * es;
     const long long l0 = (lo * es) / 8, l1 = hi > lo ? (hi * es + 7) / 8 : l0;
     if (!ll_exchange(pv, A.ll_push, A.ll_in, A.ll_stride, A.ll_flag, (const char*)A.send, bytes, l0, l1,
-                     pv.stage[pv.rank], A.ll_ustride, pv.n, pv.rank, pv.timeout_ticks, pv.err))
+                     pv.stage[pv.rank], A.ll_ustride, pv.n, pv.rank, pv.err))
       return 0;
   } else if (A.zc) {
     // zero-copy (out of place only): the operands are the ranks' sendbufs

@@ -49,5 +49,8 @@ int occupancy_vx(int n);    // vx_kernel likewise
 hipError_t launch_vx(dim3 grid, hipStream_t s, const VArgs& a);
 hipError_t launch_xfer(hipStream_t s, const XferArgs& a);
 hipError_t launch_pack(hipStream_t s, const PackArgs& a);
+// read-only stream of nin (1, 2, 4, 8) buffers of `bytes` each (copy.hip; the
+// per-box ceiling of config 2)
+hipError_t launch_read_probe(const void* const* in, int nin, long long bytes, void* sink, hipStream_t s);
 
 }  // namespace mpigx

@@ -258,7 +258,7 @@ void apply_incoming(mpigx_win* w) {
 int spin_progress(mpigx_win* w, Deadline& d) {
   rt::progress_all(w->c);
   if (d.expired()) {
-    w->c->broken = true;
+    rt::comm_mark_broken(w->c);
     return MPIGX_ERR_OTHER;
   }
   return MPIGX_SUCCESS;

@@ -15,7 +15,7 @@ namespace mpigx {
 // ---------------------------------------------------------------------------
 // shm block (one per communicator, mapped by every rank)
 // ---------------------------------------------------------------------------
-constexpr uint64_t kMagic = 0x6d70696778763034ull;  // "mpigxv04"
+constexpr uint64_t kMagic = 0x6d70696778763035ull;  // "mpigxv05"
 
 constexpr uint64_t kSigCanary = 0x6d70696778c0ffeeull;  // signal-array canary (mpigx.cpp comm_init)
 
@@ -41,6 +41,14 @@ struct ShmRank {
   unsigned long long ll_bytes;   // LL area size (0: none; must agree on every rank)
   unsigned long long ll_ptr;
   hipIpcMemHandle_t ll_h;
+  // liveness of the rank's side of the protocol, read by its peers' host
+  // waits (mpigx.cpp finish / host_allgather_wait): `broken` = its
+  // communicator failed (it will never join another collective), `kseq_enq`
+  // = the last collective launch it enqueued, `kseq_run` = the last one its
+  // device reported started (kernels' `started` word)
+  std::atomic<int> broken;
+  std::atomic<uint64_t> kseq_enq;
+  std::atomic<uint64_t> kseq_run;
   // host control-plane exchange (host_allgather): double-buffered blobs
   std::atomic<uint64_t> xseq;
   char xbuf[2][256];
@@ -170,6 +178,13 @@ struct mpigx_comm {
   // completion counter for blocking calls (host-pinned; kernels add 1 per block)
   volatile unsigned long long* done = nullptr;
   unsigned long long* done_dev = nullptr;
+  // late-peer protocol (PeerView.started / .cancel): the launch my GPU last
+  // reported started, and the word that makes a blocking launch give up
+  volatile unsigned long long* started = nullptr;
+  unsigned long long* started_dev = nullptr;
+  volatile unsigned* cancel = nullptr;
+  unsigned* cancel_dev = nullptr;
+  unsigned long long kseq = 0;  // collective launches so far (the same on every rank)
   unsigned long long done_target = 0;  // launch sequence the host waits for
   unsigned long long* dcount_dev = nullptr;
   unsigned long long dcount_total = 0;  // blocks counted on dcount so far
@@ -181,6 +196,7 @@ struct mpigx_comm {
   struct LocalReg {
     unsigned long long id;
     char* base;
+    size_t size;  // allocation size (a reallocation at the same base with another size is another allocation)
     hipIpcMemHandle_t h;
   };
   struct Import {
@@ -206,6 +222,8 @@ struct mpigx_comm {
     unsigned serial[mpigx::kMaxRanks];      // every rank's registration serial
     const char* ps[mpigx::kMaxRanks];       // every rank's sendbuf, mapped here
     char* pr[mpigx::kMaxRanks];             // every rank's recvbuf, mapped here
+    long long as[mpigx::kMaxRanks];         // bytes of each rank's send / recv allocation from the pointer
+    long long ar[mpigx::kMaxRanks];         // to its end (exported sizes; kernels check remote stores against them)
     unsigned long long tick;
   };
   std::vector<ZcTuple> ztuples;
@@ -254,6 +272,8 @@ struct mpigx_comm {
   int share_headroom = -1;              // MPIGX_SHARE_HEADROOM: ranks sharing a device leave one block per CU free (-1 auto: >= 4 ranks)
   bool scan_pp = true;                  // MPIGX_SCAN_PP: pull-push Scan / Exscan (kernels.hpp scan_pp_body)
   bool shared_gate = true;              // MPIGX_SHARED_GATE: ranks sharing a device meet on the host first
+  int peer_mem = 0;                     // MPIGX_PEER_MEM: 0 auto (memory type per pair), 1 xdev (every peer as
+                                        // if on another GPU: uncached signal / LL arrays; test knob)
   bool diag_trace = false;              // MPIGX_DIAG_TRACE: one stderr line per launch (diagnostic)
   unsigned ll_gen = 0;                  // LL flag generation (epoch >> 31) the LL area was cleared for
   int test_import_fail = 0;             // MPIGX_TEST_IMPORT_FAIL: fail that many peer imports (tests)
@@ -264,6 +284,7 @@ namespace mpigx {
 namespace rt {
 // mpigx.cpp
 int comm_check(mpigx_comm* c);
+void comm_mark_broken(mpigx_comm* c);  // broken, and published to the peers (ShmRank.broken)
 int dtype_size(int datatype);  // bytes, or -1 if not a valid datatype handle
 bool export_buf(mpigx_comm* c, const void* p, unsigned long long* id, long long* off, hipIpcMemHandle_t* h);
 char* import_buf(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemHandle_t& h);

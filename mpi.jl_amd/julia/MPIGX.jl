@@ -67,19 +67,35 @@ const DeviceOrSentinel = Union{ROCBuffer,SentinelPtr}
 # engine communicators, created collectively on first device use of a Comm;
 # the 128-byte unique id travels over host MPI (MPI.Bcast!)
 # ---------------------------------------------------------------------------
-# Keyed by the Comm OBJECT, not its handle value: MPICH hands a freed
-# communicator's handle value to the next new one, which must not inherit a
-# stale engine communicator.  Weak keys: the engine goes with its Comm — a
-# finalizer releases it locally (mpigx_comm_release: no barrier, safe once
-# this rank's last collective on it returned, so a GC finalizer may run it,
-# like comm.jl's finalizer(free, newcomm)); MPI.free(comm) sets comm.val to
-# COMM_NULL, after which engine(comm) refuses the Comm.
-const ENGINE = WeakKeyDict{Comm,Ptr{Cvoid}}()
+# Keyed by the Comm OBJECT's identity (objectid), not by its handle value or
+# by `==`: MPICH hands a freed communicator's handle value to the next new
+# one, which must not inherit a stale engine communicator, and MPI.jl's Comm
+# defines `==` by handle value (src/handle.jl:29-31) while keeping the
+# identity hash, so a Dict/WeakKeyDict keyed by Comm mixes the two (after
+# MPI.free every freed Comm `==` every other).  Each entry keeps a WeakRef to
+# its Comm: an objectid reused by a later Comm (the old one collected) finds
+# an entry whose ref is no longer that object, and drops it.
+#
+# Release (like comm.jl:85 `finalizer(free, newcomm)`): the Comm's GC
+# finalizer releases its engine communicator locally (mpigx_comm_release: no
+# barrier, safe once this rank's last collective on it returned).  A
+# finalizer runs inside whatever task allocated, possibly one that holds
+# ENGINE_LOCK, so it takes no lock and touches no Dict: it flips the entry's
+# atomic `released` flag (whoever flips it first — the finalizer or
+# __finalize at exit — does the release, exactly once) and engine() purges
+# released or collected entries under the lock.  MPI.free(comm) sets comm.val
+# to COMM_NULL, after which engine(comm) refuses the Comm.
+mutable struct EngineEntry
+    ref::WeakRef
+    handle::Ptr{Cvoid}
+    released::Threads.Atomic{Bool}
+end
+const ENGINE = Dict{UInt,EngineEntry}()
+const ENGINE_LOCK = ReentrantLock()
 
-function _engine_release(comm::Comm)
-    h = pop!(ENGINE, comm, C_NULL)
-    if h != C_NULL
-        ccall((:mpigx_comm_release, libmpigx), Cint, (Ptr{Cvoid},), h)
+function _engine_release(e::EngineEntry)
+    if !Threads.atomic_cas!(e.released, false, true)
+        ccall((:mpigx_comm_release, libmpigx), Cint, (Ptr{Cvoid},), e.handle)
         MPI.refcount_dec()
     end
     nothing
@@ -87,7 +103,15 @@ end
 
 function engine(comm::Comm)
     comm.val == MPI.COMM_NULL.val && throw(MPI.MPIError(Cint(5)))  # MPI_ERR_COMM (MPICH mpi.h): a freed Comm
-    get!(ENGINE, comm) do
+    key = objectid(comm)
+    lock(ENGINE_LOCK) do
+        e = get(ENGINE, key, nothing)
+        if e !== nothing && (e.ref.value !== comm || e.released[])
+            delete!(ENGINE, key)  # another (collected) Comm's entry at a reused objectid
+            e = nothing
+        end
+        e === nothing || return e.handle
+        filter!(kv -> kv.second.ref.value !== nothing && !kv.second.released[], ENGINE)
         id = zeros(UInt8, 128)
         rank = MPI.Comm_rank(comm)
         if rank == 0
@@ -103,8 +127,12 @@ function engine(comm::Comm)
         @mpichk ccall((:mpigx_comm_init_rank, libmpigx), Cint, (Ptr{Ptr{Cvoid}}, Cint, Ptr{UInt8}, Cint, Cint),
                       h, MPI.Comm_size(comm), id, rank, device)
         MPI.refcount_inc()  # released before MPI_Finalize (refcount_dec in _engine_release)
-        comm === MPI.COMM_WORLD || comm === MPI.COMM_SELF || finalizer(_engine_release, comm)
-        h[]
+        e = EngineEntry(WeakRef(comm), h[], Threads.Atomic{Bool}(false))
+        ENGINE[key] = e
+        if !(comm === MPI.COMM_WORLD || comm === MPI.COMM_SELF)
+            finalizer(_ -> _engine_release(e), comm)  # lock-free (see above)
+        end
+        e.handle
     end
 end
 
@@ -578,8 +606,11 @@ function DeviceOp(f, ::Type{T}; iscommutative=false) where T
 end
 
 function __finalize()
-    for comm in collect(keys(ENGINE))
-        _engine_release(comm)
+    lock(ENGINE_LOCK) do
+        for e in collect(values(ENGINE))
+            _engine_release(e)  # skipped for entries a finalizer already released
+        end
+        empty!(ENGINE)
     end
 end
 # MPI.jl 0.14 has init hooks but no finalize hooks (environment.jl:26-62):

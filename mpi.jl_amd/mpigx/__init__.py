@@ -6,7 +6,7 @@ Exscan_, SUM/MAX/..., Op, Datatype, Buffer, IN_PLACE, MPIError) over
 libmpigx.so for device-resident (ROCm) buffers.
 """
 from . import consts
-from ._lib import HEADER_PATH, LIB_PATH, lib
+from ._lib import DIAG_HEADER_PATH, HEADER_PATH, LIB_PATH, lib
 from .api import *  # noqa: F401,F403
 from .p2p import *  # noqa: F401,F403
 from .rma import *  # noqa: F401,F403

@@ -1,4 +1,4 @@
-"""ctypes binding of libmpigx.so (include/mpigx.h).
+"""ctypes binding of libmpigx.so (include/mpigx.h + include/mpigx_diag.h).
 
 The library is built in-tree (mpi.jl_amd/lib/libmpigx.so, see
 mpi.jl_amd/csrc/Makefile).  There is no fallback: if the shared object is
@@ -12,6 +12,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPIGX_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libmpigx.so"))
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "mpigx.h")
+# diagnostic exports (phase stamps, slot / mapping checks, tuner statistics,
+# probes): not part of the MPI-facing ABI
+DIAG_HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "mpigx_diag.h")
 
 _lib = None
 
@@ -54,6 +57,8 @@ PROTOTYPES = {
     "mpigx_comm_diag_slots": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     "mpigx_comm_diag_mapcheck": (c_int, [c_void_p, ctypes.c_ulonglong, c_void_p]),
     "mpigx_comm_diag_state": (c_int, [c_void_p, c_void_p]),
+    "mpigx_comm_diag_break": (c_int, [c_void_p]),
+    "mpigx_comm_diag_peer_mem": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint)]),
     "mpigx_comm_zc_stats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]),
     "mpigx_comm_host_stats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "mpigx_comm_ar_choice": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double),
@@ -61,6 +66,7 @@ PROTOTYPES = {
     "mpigx_comm_ar_costs": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double)]),
     "mpigx_comm_tune_class": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double)]),
     "mpigx_comm_probe": (c_int, [c_void_p, c_int, c_longlong, ctypes.POINTER(ctypes.c_double)]),
+    "mpigx_read_probe": (c_int, [ctypes.POINTER(c_void_p), c_int, c_longlong, c_void_p, c_void_p]),
     "mpigx_barrier": (c_int, [c_void_p]),
     "mpigx_bcast": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "mpigx_allgather": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),

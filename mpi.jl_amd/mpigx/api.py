@@ -559,7 +559,7 @@ def set_reduce_order(comm: Comm, order: int):
 KNOBS = {"ALGO": 0, "BCAST": 1, "RING_CHANNELS": 2, "MAX_BLOCKS": 3, "ONESHOT_MAX": 4, "ZC_MIN": 5,
          "BCAST_SAG_MIN": 6, "ZC_REQUIRE": 7, "BYTES_PER_BLOCK": 8, "LL_AUTO": 9, "AR_TUNE": 10,
          "ZC_OPTIMISTIC": 11, "SYNC_SPIN": 12, "STAGING_BYTES": 13, "LL_MAX": 14, "AR_SLICES": 15,
-         "SCAN_PP": 16, "SHARE_HEADROOM": 17, "SHARED_GATE": 18}
+         "SCAN_PP": 16, "SHARE_HEADROOM": 17, "SHARED_GATE": 18, "PEER_MEM": 19}
 ALGOS = {None: 0, "": 0, "auto": 0, "ll": 1, "ll2": 2, "oneshot": 3, "twoshot": 4, "push": 5, "ring": 6,
          "pull": 7, "pull_generic": 8, "pullpush": 9}
 BCAST_MODES = {None: 0, "": 0, "auto": 0, "direct": 1, "sag": 2, "relay": 3}
@@ -587,6 +587,15 @@ def get_knob(comm: Comm, knob) -> int:
     v = ctypes.c_longlong(0)
     _check(lib().mpigx_comm_get_knob(comm.val, _knob_id(knob), ctypes.byref(v)))
     return v.value
+
+
+def peer_memory(comm: Comm):
+    """(rw_mask, same_device_mask): bit q of rw_mask = rank q writes my
+    ordinary-memory signal array / LL area (same-GPU protocol); clear = the
+    uncached, cross-GPU protocol (every peer under MPIGX_PEER_MEM=xdev)."""
+    rw, sd = ctypes.c_uint(0), ctypes.c_uint(0)
+    _check(lib().mpigx_comm_diag_peer_mem(comm.val, ctypes.byref(rw), ctypes.byref(sd)))
+    return rw.value, sd.value
 
 
 def device_share(comm: Comm):

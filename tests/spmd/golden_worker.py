@@ -525,8 +525,9 @@ def main():
         R.fail += R2.fail
         R.ran += R2.ran
     MPI.Barrier(comm)
+    pm = list(MPI.peer_memory(comm))  # signalling protocol per peer pair (rw_mask, same_device)
     MPI.Finalize()
-    print(json.dumps({"rank": R.r, "n": R.n, "checks": R.ran, "failures": [str(f) for f in R.fail[:20]],
+    print(json.dumps({"rank": R.r, "n": R.n, "peer_mem": pm, "checks": R.ran, "failures": [str(f) for f in R.fail[:20]],
                       "nfail": len(R.fail)}), flush=True)
     sys.exit(1 if R.fail else 0)
 

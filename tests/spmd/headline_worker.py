@@ -213,8 +213,9 @@ def main():
             del out, rout, pref
         del mine
     MPI.Barrier(comm)
+    pm = list(MPI.peer_memory(comm))  # signalling protocol per peer pair (rw_mask, same_device)
     MPI.Finalize()
-    print(json.dumps({"rank": r, "n": n, "nfail": len(fails), "failures": [str(f) for f in fails[:20]]}), flush=True)
+    print(json.dumps({"rank": r, "n": n, "peer_mem": pm, "nfail": len(fails), "failures": [str(f) for f in fails[:20]]}), flush=True)
     sys.exit(1 if fails else 0)
 
 

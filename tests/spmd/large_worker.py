@@ -110,8 +110,9 @@ def main():
         del send
     with_knobs({})
     MPI.Barrier(comm)
+    pm = list(MPI.peer_memory(comm))  # signalling protocol per peer pair (rw_mask, same_device)
     MPI.Finalize()
-    print(json.dumps({"rank": r, "n": n, "cases": len(cases), "checked": checked, "nfail": len(fails),
+    print(json.dumps({"rank": r, "n": n, "peer_mem": pm, "cases": len(cases), "checked": checked, "nfail": len(fails),
                       "failures": [str(f) for f in fails[:20]]}), flush=True)
     sys.exit(1 if fails else 0)
 

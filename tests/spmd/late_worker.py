@@ -1,15 +1,22 @@
-"""SPMD worker: a rank that reaches a collective late, or never (ranks
-sharing one GPU, so every launch goes through the host gate, mpigx.cpp
-shared_gate).
+"""SPMD worker: a rank that reaches a collective late, or never.  With the
+host gate (ranks sharing one GPU, mpigx.cpp shared_gate) the early ranks wait
+on the host; with MPIGX_SHARED_GATE=0 (and MPIGX_PEER_MEM=xdev: the
+one-rank-per-GPU protocol) their kernels wait on the device while their hosts
+watch the peers (mpigx.cpp finish, PeerView.cancel).
 
 * late — the last rank sleeps on the host for 2.5 x MPIGX_TIMEOUT_MS before
-  a 16 MiB zero-copy Allreduce; the others are already in it.  MPI semantics:
-  the call waits for it and every rank gets the exact sum (the gate holds the
-  early ranks on the host, so no device barrier times out).  A second call
-  right after must be exact too.
+  a 16 MiB zero-copy Allreduce (`late`) or a 4 KiB one (`late_small`, the LL
+  step / staged one-shot); the others are already in it.  MPI semantics
+  (collective.jl:698-700 blocks until every rank arrives): the call waits for
+  it and every rank gets the exact sum.  A second call right after must be
+  exact too.
 * gone — after one good call the last rank exits without finalizing; the
   others' next Allreduce must fail (MPIError) within seconds instead of
   waiting for ever.
+* broken — after one good call the last rank's communicator fails
+  (mpigx_comm_diag_break, a fault injection) and its next call returns
+  MPI_ERR_OTHER at once; the others' next Allreduce must fail within seconds
+  too (ShmRank.broken), not wait for a rank that will never come.
 Launched by tests/test_late_rank_gpu.py.
 """
 import json
@@ -42,7 +49,10 @@ def main():
     MPI.Allreduce_(send, recv, MPI.SUM, comm)
     if not bool((recv == want).all()):
         fails.append("first call")
-    if scenario == "late":
+    out["peer_mem"] = list(MPI.peer_memory(comm))
+    if scenario in ("late", "late_small"):
+        if scenario == "late_small":
+            send, recv = send[:1024].clone(), recv[:1024].clone()
         if r == n - 1:
             time.sleep(2.5 * timeout_s)
         recv.fill_(-1)
@@ -57,6 +67,28 @@ def main():
             fails.append("call after")
         MPI.Barrier(comm)
         MPI.Finalize()
+    elif scenario == "broken":
+        if r == n - 1:
+            MPI.lib().mpigx_comm_diag_break(comm.val)
+            try:
+                MPI.Allreduce_(send, recv, MPI.SUM, comm)
+                fails.append("no error on the broken rank")
+            except MPI.MPIError:
+                pass
+            out["fails"] = fails
+            print(json.dumps(out), flush=True)
+            os._exit(1 if fails else 0)
+        t0 = time.time()
+        try:
+            MPI.Allreduce_(send, recv, MPI.SUM, comm)
+            fails.append("no error with a broken peer")
+        except MPI.MPIError as e:
+            out["error"] = str(e)
+        out["broken_call_s"] = round(time.time() - t0, 3)
+        torch.cuda.synchronize()
+        out["fails"] = fails
+        print(json.dumps(out), flush=True)
+        os._exit(1 if fails else 0)
     elif scenario == "gone":
         if r == n - 1:
             sys.stdout.flush()

@@ -128,8 +128,9 @@ def main():
             fails.append(("alltoall", it, rc))
     MPI.Barrier(comm)
     hits, exch = stats(L, comm)
+    pm = list(MPI.peer_memory(comm))  # signalling protocol per peer pair (rw_mask, same_device)
     MPI.Finalize()
-    print(json.dumps({"rank": r, "n": n, "nfail": len(fails), "failures": [str(f) for f in fails[:20]],
+    print(json.dumps({"rank": r, "n": n, "peer_mem": pm, "nfail": len(fails), "failures": [str(f) for f in fails[:20]],
                       "host_cost": out, "hits": hits, "exchanges": exch}), flush=True)
     sys.exit(1 if fails else 0)
 

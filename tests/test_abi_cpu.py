@@ -22,9 +22,29 @@ def header_text():
         return f.read()
 
 
-def declared_functions():
-    txt = re.sub(r"/\*.*?\*/", "", header_text(), flags=re.S)
-    return sorted(set(re.findall(r"^\s*int\s+(mpigx_\w+)\s*\(", txt, flags=re.M)))
+def declared_functions(path=None):
+    """Functions of the MPI-facing header and the diagnostic one together
+    (or of one header, `path`)."""
+    paths = [path] if path else [mpigx.HEADER_PATH, mpigx.DIAG_HEADER_PATH]
+    out = set()
+    for p in paths:
+        with open(p) as f:
+            txt = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+        out |= set(re.findall(r"^\s*int\s+(mpigx_\w+)\s*\(", txt, flags=re.M))
+    return sorted(out)
+
+
+def test_diagnostics_live_outside_the_mpi_facing_header():
+    """the diagnostic exports (phase stamps, slot and
+    mapping checks, tuner statistics, probes) are declared in
+    include/mpigx_diag.h, not in the MPI-facing include/mpigx.h."""
+    public = declared_functions(mpigx.HEADER_PATH)
+    diag = declared_functions(mpigx.DIAG_HEADER_PATH)
+    assert not set(public) & set(diag)
+    assert not [f for f in public if "_diag_" in f or (f.startswith("mpigx_comm_") and f.endswith(
+        ("_stats", "_stamps", "_probe")))], public
+    assert {"mpigx_comm_diag_slots", "mpigx_comm_diag_state", "mpigx_comm_diag_mapcheck",
+            "mpigx_comm_set_stamps"} <= set(diag)
 
 
 def header_defines():

@@ -1,7 +1,14 @@
-"""A rank that reaches a collective late or never, ranks sharing one GPU
-(tests/spmd/late_worker.py): a late rank is waited for (MPI semantics, past
-MPIGX_TIMEOUT_MS, exact results); a vanished one fails the waiting ranks'
-call within seconds instead of hanging them."""
+"""A rank that reaches a collective late or never (tests/spmd/late_worker.py):
+a late rank is waited for (MPI semantics, collective.jl:698-700: past
+MPIGX_TIMEOUT_MS, exact results); a vanished one, or one whose communicator
+failed, fails the waiting ranks' call within seconds instead of hanging them.
+
+Two configurations: `gate` — ranks sharing the GPU meet on the host first
+(shared_gate, the test-box default); `xdev` — no gate and the cross-GPU
+signalling (MPIGX_PEER_MEM=xdev), i.e. what a rank on its own GPU runs: the
+early ranks' KERNELS wait, their hosts watch the peers and cancel the wait
+only for a dead or broken peer (mpigx.cpp finish, PeerView.cancel; VERDICT
+r04 item 2)."""
 import json
 import os
 
@@ -12,6 +19,8 @@ from spmd_launch import ROOT, launch
 pytestmark = pytest.mark.gpu
 
 ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS": "2000"}
+XDEV = dict(ENV, MPIGX_SHARED_GATE="0", MPIGX_PEER_MEM="xdev")
+CONFIGS = {"gate": ENV, "xdev": XDEV}
 WORKER = os.path.join(ROOT, "tests", "spmd", "late_worker.py")
 
 
@@ -19,9 +28,10 @@ def _results(outs):
     return [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"scenario"' in l]
 
 
-@pytest.mark.parametrize("n", [2, 4])
-def test_late_rank_is_waited_for(n):
-    rcs, outs = launch(WORKER, n, timeout=240, extra_env=ENV, args=("late",))
+@pytest.mark.parametrize("cfg,n,scenario", [("gate", 2, "late"), ("gate", 4, "late"), ("xdev", 2, "late"),
+                                             ("xdev", 2, "late_small"), ("xdev", 3, "late")])
+def test_late_rank_is_waited_for(cfg, n, scenario):
+    rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=(scenario,))
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-2000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     assert all(rc == 0 for rc in rcs), msg
     res = _results(outs)
@@ -30,11 +40,27 @@ def test_late_rank_is_waited_for(n):
     assert min(early) >= 2.0 * 2.0, res  # they waited past their 2 s timeout
 
 
-def test_vanished_rank_fails_the_call():
+@pytest.mark.parametrize("cfg", ["gate", "xdev"])
+def test_vanished_rank_fails_the_call(cfg):
     n = 3
-    rcs, outs = launch(WORKER, n, timeout=240, extra_env=ENV, args=("gone",))
+    rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=("gone",))
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-2000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     res = _results(outs)
     assert len(res) == n - 1, msg
     assert all(not x["fails"] and x["gone_call_s"] < 30 for x in res), res
     assert all(rc == 0 for rc in rcs[: n - 1]), msg
+
+
+@pytest.mark.parametrize("cfg", ["gate", "xdev"])
+def test_broken_peer_fails_the_call(cfg):
+    """a rank whose communicator already failed never reaches the
+    gate or launches; its peers learn it from the shm block (ShmRank.broken)
+    and fail within seconds instead of waiting for it."""
+    n = 3
+    rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=("broken",))
+    msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-2000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
+    res = _results(outs)
+    assert len(res) == n, msg
+    assert all(not x["fails"] for x in res), res
+    assert all(x["broken_call_s"] < 30 for x in res if x["rank"] != n - 1), res
+    assert all(rc == 0 for rc in rcs), msg
