@@ -178,7 +178,7 @@ struct PeerView {
   unsigned args_sum;
 };
 // Checksum of an argument block (host and device; mpigx.cpp seal_args,
-// device.hpp args_intact): word i mixed with its index, summed — a permuted,
+// device.hpp args_fault): word i mixed with its index, summed — a permuted,
 // stale or partly overwritten block does not match.
 __host__ __device__ inline unsigned args_mix(unsigned w, unsigned i) {
   unsigned x = w ^ (i * 0x9E3779B9u);

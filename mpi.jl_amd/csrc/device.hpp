@@ -1095,7 +1095,7 @@ __device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t e
 // verdict — a separate flag word raced the completion store over PCIe.
 //
 // Before the barrier (round 5): the argument block must be
-// the one the host sealed for THIS launch — its checksum (args_intact) and,
+// the one the host sealed for THIS launch — its checksum (args_fault) and,
 // for blocking launches, its completion base: at entry the device counter
 // holds every earlier launch's blocks and at most this launch's own, so a
 // stale block (an older launch's arguments) shows.  A zero-copy kernel
@@ -1106,8 +1106,12 @@ __device__ __forceinline__ bool rank_barrier_grid(const PeerView& pv, uint64_t e
 // leaves; its host breaks the communicator and says so in the shm block, and
 // every peer's host then cancels its own wait (mpigx.cpp finish), so all
 // ranks fail the call instead of one rank faulting the GPU.
-__device__ __noinline__ bool args_intact(const PeerView& pv, unsigned* why) {
-  __shared__ unsigned s_sum, s_ok;
+// Returns 0 when the block is intact, 1 = checksum mismatch, 2 = stale
+// (another launch's completion base).  By value, not through an out pointer:
+// a pointer to the caller's local would put that local on a stack, i.e. give
+// every collective kernel a private segment (tests/test_kernel_resources_cpu.py).
+__device__ __noinline__ unsigned args_fault(const PeerView& pv) {
+  __shared__ unsigned s_sum, s_why;
   if (threadIdx.x == 0) s_sum = 0;
   __syncthreads();
   const unsigned nw = pv.args_words;
@@ -1120,24 +1124,20 @@ __device__ __noinline__ bool args_intact(const PeerView& pv, unsigned* why) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned ok = (nw == 0 || s_sum == pv.args_sum) ? 1u : 0u;
-    *why = ok ? 0u : 1u;
-    if (ok && pv.done) {
+    unsigned why = (nw == 0 || s_sum == pv.args_sum) ? 0u : 1u;
+    if (!why && pv.done) {
       const unsigned long long c = __hip_atomic_load(pv.dcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (c < pv.dbase || c >= pv.dbase + gridDim.x) {
-        ok = 0u;
-        *why = 2u;
-      }
+      if (c < pv.dbase || c >= pv.dbase + gridDim.x) why = 2u;
     }
-    s_ok = ok;
+    s_why = why;
   }
   __syncthreads();
-  return s_ok != 0;
+  return s_why;
 }
 
 __device__ __forceinline__ bool zc_enter(const PeerView& pv, uint64_t ep, int* abort, bool strict = true) {
-  unsigned why = 0;
-  if (!args_intact(pv, &why)) {
+  const unsigned why = args_fault(pv);
+  if (why) {
     if (threadIdx.x == 0) {
       __hip_atomic_store(pv.err, kErrProtocol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (pv.stamps) pv.stamps[(size_t)blockIdx.x * 8 + 6] = 0xA765000000000000ull | why;

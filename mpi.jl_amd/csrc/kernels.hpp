@@ -282,8 +282,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     const char* srcs[NMAX];
     long long lens[NMAX];
     {  // phase 1 stores into the peers' arenas before any barrier (zc_enter's checks)
-      unsigned why = 0;
-      if (!args_intact(pv, &why)) {
+      if (args_fault(pv)) {
         if (tid == 0) __hip_atomic_store(pv.err, kErrProtocol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return 0;
       }

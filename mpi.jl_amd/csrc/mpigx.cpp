@@ -909,7 +909,7 @@ void zc_apply(PeerView& pv, const ZcLaunch& z) {
   pv.zc_bad = z.bad;
 }
 
-// Seals a zero-copy launch's argument block (device.hpp args_intact): its
+// Seals a zero-copy launch's argument block (device.hpp args_fault): its
 // size in words and the checksum of those words with args_sum itself 0.
 // The block must be complete (and its padding zero: every caller memsets it).
 template <class Args>
@@ -3559,11 +3559,13 @@ static int scan_common(const void* sendbuf, void* recvbuf, int count, int dataty
   // and written by one thread of its owner only; n > 8 keeps the pull
   // schedule, out of place (with IN_PLACE my recvbuf, which I overwrite,
   // would be the operand the higher ranks read)
-  // OFF by default since round 3: at n = 8 ranks on one GPU the pull-push
-  // scan raised an illegal memory access in the 64 Mi-element headline case
-  // (and returned wrong words on one rank in another run) while n = 2 and 4
-  // were green; cause not found yet.  Its remote stores are the
-  // only difference from the pull schedule below, which every test covers.
+  // On by default (agreed knob MPIGX_SCAN_PP, c->scan_pp = 1).  Round 3 saw
+  // one aperture violation (n = 8 ranks on one GPU, 64 Mi-element headline
+  // case) and wrong words on one rank in another run; since round 5 the
+  // kernel checks its argument block (checksum + launch freshness) and every
+  // load / store extent against the view's exported allocation sizes before
+  // touching a peer's buffer, and a failed check aborts every rank's launch
+  // (DESIGN §13 "The round-3 aperture violation").
   const bool pp = c->scan_pp && c->n <= 8;
   if ((pp || sendbuf != MPIGX_IN_PLACE) && c->zc_min > 0 && (long long)count * es >= c->zc_min) {
     // zero-copy: no copy-in, no rounds

@@ -5,7 +5,18 @@ sequence at n ranks.  Per-block stamps are on for every call: when a call
 fails, every rank prints its blocks' entry times (device wall clock, 100 MHz,
 one clock for all ranks of a GPU) and the per-block timeout records (epoch
 awaited, word last seen, the peer, when the block gave up) so that the ranks'
-records line up in time."""
+records line up in time.
+
+Modes (one script since round 5; round 4's separate variant is in history at
+commit 8a5ba8c):
+  REPRO_COMPARE=equal    (default) torch.equal compares between the calls
+  REPRO_COMPARE=nonzero  round 3's `(out != exp).nonzero()` compares: with 8
+                         processes on one GPU they take tens of seconds
+                         (rocPRIM look-back scans time-sliced, DESIGN §12
+                         "n = 8 stall") and rank 0, which has no Exscan result
+                         to compare, reaches the Reduce that much earlier
+  REPRO_WATCH=1          a thread reporting, after every 4 s without progress,
+                         where the rank is (mpigx_comm_diag_state)"""
 import ctypes
 import json
 import os
@@ -54,6 +65,33 @@ def main():
                               "timeouts_b_ep_seen_lane_tgiveup_rmw_nt_acq": tmo}), flush=True)
             sys.exit(1)
 
+    nonzero = os.environ.get("REPRO_COMPARE", "equal") == "nonzero"
+
+    def same(out, exp):
+        if nonzero:
+            return (out != exp).nonzero().numel() == 0
+        return torch.equal(out, exp)
+
+    if os.environ.get("REPRO_WATCH") and hasattr(L, "mpigx_comm_diag_state"):
+        import threading
+        main_t = threading.main_thread()
+
+        def watch():
+            last = None
+            while main_t.is_alive():
+                time.sleep(4.0)
+                st8 = (ctypes.c_ulonglong * 8)()
+                L.mpigx_comm_diag_state(comm.val, st8)
+                cur = tuple(st8)
+                if cur == last:  # nothing moved for 4 s: say where the rank is
+                    frame = sys._current_frames().get(main_t.ident)
+                    where = f"{frame.f_code.co_name}:{frame.f_lineno}" if frame else "?"
+                    print(json.dumps({"watch": r, "t": round(time.time(), 3), "at": where, "state": list(cur)}),
+                          file=sys.stderr, flush=True)
+                last = cur
+
+        threading.Thread(target=watch, daemon=True).start()
+
     ops = (("BAND", MPI.BAND, torch.bitwise_and), ("BOR", MPI.BOR, torch.bitwise_or), ("MAX", MPI.MAX, torch.maximum))
     nbad = 0
     for tdt, lim in ((torch.int32, 1 << 31), (torch.int64, 1 << 62)):
@@ -72,11 +110,11 @@ def main():
                 out = torch.zeros_like(mine)
                 print(f"r{r} {tdt} {oname} scan t={time.time():.3f}", file=sys.stderr, flush=True)
                 run(f"{tdt} {oname} scan", lambda: MPI.Scan_(mine, out, op, comm))
-                nbad += int(not torch.equal(out, pref))
+                nbad += int(not same(out, pref))
                 out.fill_(7)
                 print(f"r{r} {tdt} {oname} exscan t={time.time():.3f}", file=sys.stderr, flush=True)
                 run(f"{tdt} {oname} exscan", lambda: MPI.Exscan_(mine, out, op, comm))
-                nbad += int(not torch.equal(out, ex) if r > 0 else not bool((out == 7).all()))
+                nbad += int(not same(out, ex) if r > 0 else not bool((out == 7).all()))
                 root = n - 1
                 rout = torch.zeros_like(mine) if r == root else None
                 print(f"r{r} {tdt} {oname} reduce t={time.time():.3f}", file=sys.stderr, flush=True)
@@ -85,7 +123,7 @@ def main():
                     tot = pref
                     for q in range(r + 1, n):
                         tot = fn(tot, gen(q))
-                    nbad += int(not torch.equal(rout, tot))
+                    nbad += int(not same(rout, tot))
                 del out, rout, pref, ex
         del mine
     L.mpigx_comm_set_stamps(comm.val, None)
