@@ -908,6 +908,17 @@ void zc_apply(PeerView& pv, const ZcLaunch& z) {
   pv.zc_key = z.key;
   pv.zc_bad = z.bad;
 }
+// Extents of a zero-copy byte-mover launch (Bcast / Allgather / Alltoall),
+// checked on the host against the view's exported allocation sizes — the
+// same numbers on every rank, so the same verdict everywhere: every rank's
+// region the launch reads holds `src_bytes` from the view's pointer, every
+// region it may store into `dst_bytes`.  A failure marks the launch bad, and
+// its entry barrier aborts it on every rank before any peer byte is touched
+// (ar_zc_kernel and scan_pp_body check the same sizes on the device).
+void zc_extents(PeerView& pv, const ZcLaunch& z, int n, long long src_bytes, long long dst_bytes) {
+  for (int q = 0; q < n; ++q)
+    if (z.as[q] < src_bytes || z.ar[q] < dst_bytes) pv.zc_bad = 1;
+}
 
 // Seals a zero-copy launch's argument block (device.hpp args_fault): its
 // size in words and the checksum of those words with args_sum itself 0.
@@ -2800,6 +2811,7 @@ static int bcast_impl(void* buf, int count, int datatype, int root, mpigx_comm_t
       a.bytes = bytes;
       a.recv = buf;
       for (int p = 0; p < c->n; ++p) a.zsrc[p] = z.ps[p];
+      zc_extents(a.pv, z, c->n, bytes, (relay || sag) ? bytes : 0);  // relay / sag store into peers' buffers
       int g;
       if (relay) {
         a.mode = C_BCAST_RELAY_ZC;
@@ -2911,6 +2923,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
       a.bytes = bytes;
       a.total = bytes;
       for (int p = 0; p < n; ++p) a.zsrc[p] = z.ps[p];
+      zc_extents(a.pv, z, n, bytes * n, 0);
       const int g = grid_for(c, bytes * n, cap_copy(c));
       a.slice = rup(cdiv(bytes, g), 16);
       a.send = s;
@@ -2937,6 +2950,7 @@ static int gather_like(const void* send, int scount, int stype, void* recv, int 
       a.bytes = bytes;
       a.total = bytes;
       for (int p = 0; p < n; ++p) a.zsrc[p] = z.ps[p];
+      zc_extents(a.pv, z, n, bytes, 0);
       const int g = grid_for(c, bytes, cap_copy(c));
       a.slice = rup(cdiv(bytes, g), 16);
       a.send = s;

@@ -611,9 +611,23 @@ def _stream(comm):
     lib().mpigx_comm_set_stream(comm.val, ctypes.c_void_p(s))
 
 
+class InexactError(ValueError):
+    """Julia's InexactError: a ccall argument declared `Cint` that does not
+    fit (e.g. a count of 2^31 elements, collective.jl:698-700) fails in
+    `convert(Cint, x)` before any MPI call is made."""
+
+
+def _check_cint_args(fn, args):
+    for a, t in zip(args, getattr(fn, "argtypes", None) or ()):
+        if t is ctypes.c_int and isinstance(a, int) and not -(1 << 31) <= a < (1 << 31):
+            raise InexactError(f"InexactError: trunc(Int32, {a})")
+
+
 def _call(coll, buf, comm, *args):
     """One ccall: `MPI_<coll>` in libmpi for host buffers, `mpigx_<coll>` in
-    libmpigx for device buffers — the same argument list either way."""
+    libmpigx for device buffers — the same argument list either way.  Int
+    arguments the C prototype takes as `int` must fit (Julia's Cint
+    conversion), else InexactError and no call."""
     if _is_host(buf):
         if comm.host is None:
             raise TypeError("host buffers need host libmpi (start the ranks with mpiexec)")
@@ -623,7 +637,9 @@ def _call(coll, buf, comm, *args):
         if not comm.val:
             raise TypeError("device buffers need a ROCm device")
         _stream(comm)
-        rc = getattr(lib(), "mpigx_" + coll.lower())(*args, comm.val)
+        fn = getattr(lib(), "mpigx_" + coll.lower())
+        _check_cint_args(fn, args)
+        rc = fn(*args, comm.val)
     _check(rc)
 
 

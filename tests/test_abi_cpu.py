@@ -217,3 +217,17 @@ def test_libmpi_op_carries_its_function():
     assert op.val == 0x98000001 and op.fptr is f and op.iscommutative
     assert mpigx.Op(op).fptr is f
     assert mpigx.SUM.fptr is None
+
+
+def test_count_is_a_cint():
+    """collective.jl:698-700 passes `count` as Cint: 2^31 - 1 goes through,
+    2^31 is Julia's InexactError before any call (no silent wrap to a
+    negative count in ctypes)."""
+    from mpigx import api
+    L = mpigx.lib()
+    fn = L.mpigx_allreduce
+    api._check_cint_args(fn, (None, None, (1 << 31) - 1, 0, 0))
+    api._check_cint_args(fn, (None, None, -(1 << 31), 0, 0))
+    for bad in (1 << 31, -(1 << 31) - 1, 1 << 40):
+        with pytest.raises(api.InexactError):
+            api._check_cint_args(fn, (None, None, bad, 0, 0))
