@@ -1689,8 +1689,15 @@ int host_allgather_wait(mpigx_comm* c, const void* mine, int len, void* out, boo
   }
   return MPIGX_SUCCESS;
 }
+// Every host exchange of a collective (zero-copy view agreement, the
+// v-collectives' round agreement, tuner verdicts, knob changes, RMA fences,
+// Comm_split) waits for a late rank as long as its process lives and its
+// communicator has not failed (round 5): MPI's collectives block until every
+// rank arrives (collective.jl:698-700), so a rank that spends longer than
+// MPIGX_TIMEOUT_MS in a checkpoint or a host phase before a Gatherv or a
+// stream-ordered first call must not break the communicator.
 int host_allgather(mpigx_comm* c, const void* mine, int len, void* out) {
-  return host_allgather_wait(c, mine, len, out, false);
+  return host_allgather_wait(c, mine, len, out, true);
 }
 
 // Per-rank description of a personalised exchange (see VArgs in common.hpp).

@@ -10,6 +10,12 @@ watch the peers (mpigx.cpp finish, PeerView.cancel).
   (collective.jl:698-700 blocks until every rank arrives): the call waits for
   it and every rank gets the exact sum.  A second call right after must be
   exact too.
+* late_vx — the same, before an Allgatherv (its rounds are agreed over the
+  host control plane before any launch, so the early ranks wait on the host,
+  host_allgather);
+* late_so — the same on a stream-ordered communicator with fresh 16 MiB
+  buffers (a stream-ordered zero-copy call agrees on the view over the host
+  control plane before its launch);
 * gone — after one good call the last rank exits without finalizing; the
   others' next Allreduce must fail (MPIError) within seconds instead of
   waiting for ever.
@@ -61,6 +67,34 @@ def main():
         out["late_call_s"] = round(time.time() - t0, 3)
         if not bool((recv == want).all()):
             fails.append("late call")
+        recv.fill_(-1)
+        MPI.Allreduce_(send, recv, MPI.SUM, comm)
+        if not bool((recv == want).all()):
+            fails.append("call after")
+        MPI.Barrier(comm)
+        MPI.Finalize()
+    elif scenario in ("late_vx", "late_so"):
+        if r == n - 1:
+            time.sleep(2.5 * timeout_s)
+        t0 = time.time()
+        if scenario == "late_vx":
+            counts = [1000 + 17 * q for q in range(n)]
+            mine = torch.full((counts[r],), float(r + 1), device="cuda")
+            got = torch.full((sum(counts),), -1.0, device="cuda")
+            MPI.Allgatherv_(mine, got, counts, comm)
+            exp = torch.cat([torch.full((counts[q],), float(q + 1), device="cuda") for q in range(n)])
+            if not torch.equal(got, exp):
+                fails.append("late allgatherv")
+        else:
+            MPI.api._check(MPI.lib().mpigx_comm_set_blocking(comm.val, 0))
+            send2 = torch.full((count,), float(r + 1), device="cuda")
+            recv2 = torch.full((count,), -1.0, device="cuda")
+            MPI.Allreduce_(send2, recv2, MPI.SUM, comm)
+            torch.cuda.synchronize()
+            if not bool((recv2 == want).all()):
+                fails.append("late stream-ordered call")
+            MPI.api._check(MPI.lib().mpigx_comm_set_blocking(comm.val, 1))
+        out["late_call_s"] = round(time.time() - t0, 3)
         recv.fill_(-1)
         MPI.Allreduce_(send, recv, MPI.SUM, comm)
         if not bool((recv == want).all()):

@@ -29,7 +29,8 @@ def _results(outs):
 
 
 @pytest.mark.parametrize("cfg,n,scenario", [("gate", 2, "late"), ("gate", 4, "late"), ("xdev", 2, "late"),
-                                             ("xdev", 2, "late_small"), ("xdev", 3, "late")])
+                                             ("xdev", 2, "late_small"), ("xdev", 3, "late"),
+                                             ("xdev", 2, "late_vx"), ("xdev", 2, "late_so")])
 def test_late_rank_is_waited_for(cfg, n, scenario):
     rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=(scenario,))
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-2000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
