@@ -619,6 +619,15 @@ bool zc_export(mpigx_comm* c, const void* p, char** pbase, unsigned long long* i
     (void)hipGetLastError();
     return false;
   }
+  // an allocation the loaded HIP runtime cannot map into a peer
+  // (runtime.hpp ipc_alloc_max): not exportable — zero-copy calls take the
+  // staged path on every rank, p2p stages the message in a pooled temporary
+  if (c->ipc_alloc_max > 0 && (long long)size > c->ipc_alloc_max) {
+    if (c->diag_trace)
+      fprintf(stderr, "[trace r%d] not exporting %zu-byte allocation (IPC limit %lld, HIP runtime %d)\n", c->rank,
+              size, c->ipc_alloc_max, c->hip_runtime);
+    return false;
+  }
   *pbase = (char*)base;
   *id = bid;
   *off = (const char*)p - (const char*)base;
@@ -658,6 +667,7 @@ char* zc_import(mpigx_comm* c, int peer, unsigned long long id, const hipIpcMemH
     --c->test_import_fail;
     return nullptr;
   }
+  if (c->diag_trace) fprintf(stderr, "[trace r%d] zc import peer %d id=%llu: opening\n", c->rank, peer, id);
   if (hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
@@ -810,7 +820,9 @@ int zc_exchange(mpigx_comm* c, const void* send, void* recv, ZcLaunch* z) {
   memset(z, 0, sizeof *z);
   const int n = c->n;
   ZcBlob mine;
+  if (c->diag_trace) fprintf(stderr, "[trace r%d] exchange: registering\n", c->rank);
   zc_register(c, send, recv, &mine);
+  if (c->diag_trace) fprintf(stderr, "[trace r%d] exchange: registered ok=%d serial=%u\n", c->rank, mine.ok, mine.serial);
   ZcBlob all[kMaxRanks];
   const int rc = host_allgather(c, &mine, sizeof mine, all);
   if (rc) return -rc;
@@ -884,6 +896,7 @@ int zc_run(mpigx_comm* c, const void* send, void* recv, bool* staged, F&& launch
     zc_optimistic(c, send, recv, &z);
     int rc = launch(z);
     if (!rc) rc = finish(c);
+    if (c->diag_trace) fprintf(stderr, "[trace r%d] optimistic launch finished rc=%d aborted=%d\n", c->rank, rc, c->last_aborted ? 1 : 0);
     if (rc) return rc;
     if (!zc_take_stale(c)) {
       c->zstat_hits++;
@@ -2162,6 +2175,12 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   // diagnostic only (selects no path, so not an agreed knob): one stderr line
   // per launch with its epoch, grid, view key and completion sequence
   c->diag_trace = env_ll("MPIGX_DIAG_TRACE", 0) != 0;  // per rank: fault injection, not a knob
+  // IPC export size limit (runtime.hpp ipc_alloc_max): selects no kernel —
+  // whether a buffer is exportable is agreed per exchange (zc_exchange: every
+  // rank takes the staged path if any rank cannot export)
+  (void)hipRuntimeGetVersion(&c->hip_runtime);
+  c->ipc_alloc_max = c->hip_runtime < 70200000 ? (1ll << 31) - 1 : 0;
+  c->ipc_alloc_max = env_ll("MPIGX_IPC_ALLOC_MAX", c->ipc_alloc_max);
 
   HIPCK(hipMalloc(&c->stage, c->stage_bytes));
   // rows [0, kMaxBlocks): per-block barriers; row kMaxBlocks: whole-launch

@@ -586,9 +586,24 @@ int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpi
       return MPIGX_ERR_INTERN;
     }
     if (dest != c->rank && !rt::export_buf(c, r->sbuf, &r->buf_id, &r->off, &r->h)) {
-      pack_put(r);
-      delete r;
-      return MPIGX_ERR_BUFFER;  // not a device allocation that can be IPC-exported
+      // a contiguous message in an allocation the runtime cannot IPC-map
+      // (runtime.hpp ipc_alloc_max): staged in a pooled temporary of its own
+      bool ok = false;
+      const long long rounded = (r->bytes + (1 << 20) - 1) & ~((1ll << 20) - 1);  // pack_get's allocation
+      if (!r->pack_tmp && (c->ipc_alloc_max <= 0 || rounded <= c->ipc_alloc_max)) {
+        r->pack_tmp = pack_get(P, r->bytes, &r->pack_cap);
+        if (r->pack_tmp && hipMemcpyAsync(r->pack_tmp, buf, r->bytes, hipMemcpyDeviceToDevice, c->stream) == hipSuccess &&
+            hipStreamSynchronize(c->stream) == hipSuccess) {
+          r->sbuf = r->pack_tmp;
+          ok = rt::export_buf(c, r->sbuf, &r->buf_id, &r->off, &r->h);
+        }
+        (void)hipGetLastError();
+      }
+      if (!ok) {
+        pack_put(r);
+        delete r;
+        return MPIGX_ERR_BUFFER;  // not a device allocation that can be IPC-exported
+      }
     }
   }
   P->sendq[dest].push_back(r);

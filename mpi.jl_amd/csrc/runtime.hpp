@@ -277,6 +277,13 @@ struct mpigx_comm {
   bool diag_trace = false;              // MPIGX_DIAG_TRACE: one stderr line per launch (diagnostic)
   unsigned ll_gen = 0;                  // LL flag generation (epoch >> 31) the LL area was cleared for
   int test_import_fail = 0;             // MPIGX_TEST_IMPORT_FAIL: fail that many peer imports (tests)
+  // Largest allocation this rank IPC-exports (zero-copy views, p2p, RMA);
+  // 0 = no limit.  HIP runtimes before 7.2 (e.g. the 7.0 runtime PyTorch
+  // bundles, which a torch process loads instead of the system's) never
+  // return from hipIpcOpenMemHandle of an allocation >= 2 GiB (DESIGN §13,
+  // tools/ipc_torch.py); MPIGX_IPC_ALLOC_MAX overrides (tests).
+  long long ipc_alloc_max = 0;
+  int hip_runtime = 0;                  // hipRuntimeGetVersion of the runtime this process loaded
   std::mutex mu;
 };
 

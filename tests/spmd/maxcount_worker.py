@@ -27,7 +27,7 @@ import torch  # noqa: E402
 
 import mpigx as MPI  # noqa: E402
 
-CMAX = (1 << 31) - 1
+CMAX = int(os.environ.get("MAXCOUNT_ELEMS", (1 << 31) - 1))  # smaller for diagnosis only
 
 
 def main():
@@ -35,6 +35,21 @@ def main():
     r, n = MPI.Comm_rank(comm), MPI.Comm_size(comm)
     dev = torch.device("cuda")
     fails, times = [], {}
+    if os.environ.get("MAXCOUNT_WATCH"):  # diagnosis: where a stuck call is
+        import ctypes
+        import faulthandler
+        import threading
+        faulthandler.dump_traceback_later(30, repeat=True, file=sys.stderr)
+        L = MPI.lib()
+
+        def watch():
+            while True:
+                time.sleep(5.0)
+                st8 = (ctypes.c_ulonglong * 8)()
+                L.mpigx_comm_diag_state(comm.val, st8)
+                print(f"r{r} watch {list(st8)}", file=sys.stderr, flush=True)
+
+        threading.Thread(target=watch, daemon=True).start()
 
     def i8(q, seed, count=CMAX):
         g = torch.Generator(device=dev).manual_seed(seed + 101 * q)
@@ -42,10 +57,22 @@ def main():
 
     def timed(name, fn):
         torch.cuda.synchronize()
+        print(f"r{r} {name} ...", file=sys.stderr, flush=True)
         t0 = time.time()
         fn()
         torch.cuda.synchronize()
         times[name] = round(time.time() - t0, 4)
+        print(f"r{r} {name} {times[name]} s", file=sys.stderr, flush=True)
+
+    import ctypes
+    hip_rt = ctypes.c_int(0)
+    ctypes.CDLL("libamdhip64.so").hipRuntimeGetVersion(ctypes.byref(hip_rt))
+    capped = hip_rt.value < 70200000  # runtime.hpp ipc_alloc_max: no IPC export of allocations >= 2 GiB
+
+    def zc_hits():  # launches made on an agreed zero-copy view
+        h, x = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        MPI.lib().mpigx_comm_zc_stats(comm.val, ctypes.byref(h), ctypes.byref(x))
+        return h.value
 
     # --- Allreduce int8 SUM: calls 1-4 are the zero-copy tuner's (register,
     # pull, push, pull-push), call 5 runs its choice; every call exact
@@ -59,6 +86,10 @@ def main():
         timed(f"allreduce_i8_sum_call{k + 1}", lambda: MPI.Allreduce_(x, out, MPI.SUM, comm))
         if not torch.equal(out, exp):
             fails.append(("allreduce-i8-sum", k + 1))
+    # an allocation the loaded HIP runtime cannot IPC-map goes staged on every
+    # rank: no zero-copy view was ever built for it
+    if capped and CMAX >= (1 << 31) - 1 and zc_hits() != 0:
+        fails.append(("zero-copy view over a >= 2 GiB allocation on a capped runtime", zc_hits()))
     # in place
     out.copy_(x)
     timed("allreduce_i8_sum_inplace", lambda: MPI.Allreduce_(out, MPI.SUM, comm))
@@ -72,6 +103,18 @@ def main():
     if not torch.equal(out, exp):
         fails.append(("allreduce-i8-sum-staged",))
     MPI.set_knob(comm, "ZC_MIN", zc0)
+
+    # --- point-to-point from / into the middle of the 2 GiB buffers: the
+    # sender's allocation is staged through a pooled temporary where the
+    # runtime cannot IPC-map it (p2p.cpp mpigx_isend)
+    seg = 16 << 20
+    lo = CMAX // 2 - seg // 2
+    peer = (r + 1) % n
+    src = (r - 1) % n
+    out.fill_(0)
+    timed("sendrecv_i8_16MiB_in_2GiB", lambda: MPI.Sendrecv_(x[lo:lo + seg], peer, 7, out[lo:lo + seg], src, 7, comm))
+    if not torch.equal(out[lo:lo + seg], i8(src, 10)[lo:lo + seg]):
+        fails.append(("sendrecv-in-2GiB",))
 
     # --- Reduce int8 BXOR to the last rank
     root = n - 1
@@ -119,7 +162,7 @@ def main():
     del dst, x
 
     # --- Alltoall: blocks of 2^30 elements, n·2^30 per rank (2^31 at n = 2)
-    blk = 1 << 30
+    blk = (CMAX + 1) // 2
     a2s = i8(r, 20, n * blk)
     a2r = torch.empty_like(a2s)
     timed("alltoall_i8", lambda: MPI.Alltoall_(a2s, a2r, blk, comm))
@@ -163,7 +206,8 @@ def main():
 
     MPI.Barrier(comm)
     MPI.Finalize()
-    print(json.dumps({"rank": r, "n": n, "nfail": len(fails), "fails": fails[:10], "times_s": times}), flush=True)
+    print(json.dumps({"rank": r, "n": n, "nfail": len(fails), "fails": fails[:10], "hip_runtime": hip_rt.value,
+                      "ipc_capped": capped, "times_s": times}), flush=True)
 
 
 if __name__ == "__main__":

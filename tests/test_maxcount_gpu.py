@@ -15,7 +15,7 @@ from spmd_launch import ROOT, launch
 
 pytestmark = pytest.mark.gpu
 
-ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS": "60000"}
+ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS": os.environ.get("MPIGX_TIMEOUT_MS", "60000")}
 
 
 @pytest.mark.parametrize("n", [2, 3])
