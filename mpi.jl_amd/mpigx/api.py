@@ -617,17 +617,19 @@ class InexactError(ValueError):
     `convert(Cint, x)` before any MPI call is made."""
 
 
-def _check_cint_args(fn, args):
-    for a, t in zip(args, getattr(fn, "argtypes", None) or ()):
-        if t is ctypes.c_int and isinstance(a, int) and not -(1 << 31) <= a < (1 << 31):
-            raise InexactError(f"InexactError: trunc(Int32, {a})")
+def _cint(x) -> int:
+    """`count` as MPI.jl passes it: Julia's `convert(Cint, count)`
+    (collective.jl:698-700 `ccall(..., Cint, ...)`) — InexactError, and no
+    call, when it does not fit (ctypes would wrap it to a negative count)."""
+    x = int(x)
+    if not -(1 << 31) <= x < (1 << 31):
+        raise InexactError(f"InexactError: trunc(Int32, {x})")
+    return x
 
 
 def _call(coll, buf, comm, *args):
     """One ccall: `MPI_<coll>` in libmpi for host buffers, `mpigx_<coll>` in
-    libmpigx for device buffers — the same argument list either way.  Int
-    arguments the C prototype takes as `int` must fit (Julia's Cint
-    conversion), else InexactError and no call."""
+    libmpigx for device buffers — the same argument list either way."""
     if _is_host(buf):
         if comm.host is None:
             raise TypeError("host buffers need host libmpi (start the ranks with mpiexec)")
@@ -637,9 +639,7 @@ def _call(coll, buf, comm, *args):
         if not comm.val:
             raise TypeError("device buffers need a ROCm device")
         _stream(comm)
-        fn = getattr(lib(), "mpigx_" + coll.lower())
-        _check_cint_args(fn, args)
-        rc = fn(*args, comm.val)
+        rc = getattr(lib(), "mpigx_" + coll.lower())(*args, comm.val)
     _check(rc)
 
 
@@ -732,7 +732,7 @@ def Bcast_(buf, *args):
     else:
         root, comm = args
         count = _len(buf)
-    _call("Bcast", buf, comm, _ptr(buf), int(count), _eltype(buf).val, int(root))
+    _call("Bcast", buf, comm, _ptr(buf), _cint(count), _eltype(buf).val, int(root))
     return buf
 
 
@@ -742,7 +742,7 @@ def _side(buf, count, T):
     vector type — otherwise the wrapper's count and element type."""
     if isinstance(buf, Buffer):
         return int(buf.count), buf.datatype.val
-    return int(count), T.val
+    return _cint(count), T.val
 
 
 def Allgather_(*args):
@@ -855,7 +855,7 @@ def Scatterv_(sendbuf, recvbuf, counts, root, comm):
     T = _eltype(sendbuf) if recvbuf is IN_PLACE else _eltype(recvbuf)
     data = sendbuf if recvbuf is IN_PLACE else recvbuf
     _call("Scatterv", data, comm, _ptr(sendbuf), _cints(counts), _cints(_disps(counts)), T.val, _ptr(recvbuf),
-          int(counts[rank]), T.val, int(root))
+          _cint(counts[rank]), T.val, int(root))
     return recvbuf
 
 
@@ -913,7 +913,7 @@ def Gatherv_(sendbuf, recvbuf, counts, root, comm):
     _assert_minlength(sendbuf, counts[rank])
     T = _eltype(recvbuf) if sendbuf is IN_PLACE else _eltype(sendbuf)
     data = recvbuf if sendbuf is IN_PLACE else sendbuf
-    _call("Gatherv", data, comm, _ptr(sendbuf), int(counts[rank]), T.val, _ptr(recvbuf), _cints(counts),
+    _call("Gatherv", data, comm, _ptr(sendbuf), _cint(counts[rank]), T.val, _ptr(recvbuf), _cints(counts),
           _cints(_disps(counts)), T.val, int(root))
     return recvbuf if isroot else None
 
@@ -936,7 +936,7 @@ def Allgatherv_(*args):
     _assert_minlength(recvbuf, sum(counts))
     _assert_minlength(sendbuf, sendcnt)
     T = _eltype(recvbuf)
-    _call("Allgatherv", recvbuf, comm, _ptr(sendbuf), int(sendcnt), T.val, _ptr(recvbuf), _cints(counts),
+    _call("Allgatherv", recvbuf, comm, _ptr(sendbuf), _cint(sendcnt), T.val, _ptr(recvbuf), _cints(counts),
           _cints(_disps(counts)), T.val)
     return recvbuf
 
@@ -1006,7 +1006,7 @@ def Reduce_(*args):
     data = recvbuf if sendbuf is IN_PLACE else sendbuf
     T = _eltype(data)
     opx = _as_op(op, _dtype(data))
-    _call("Reduce", data, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val, _op_val(opx, data), int(root))
+    _call("Reduce", data, comm, _ptr(sendbuf), _ptr(recvbuf), _cint(count), T.val, _op_val(opx, data), int(root))
     return recvbuf
 
 
@@ -1041,7 +1041,7 @@ def Allreduce_(*args):
         assert _eltype(sendbuf) == _eltype(recvbuf)
     T = _eltype(recvbuf)
     opx = _as_op(op, _dtype(recvbuf))
-    _call("Allreduce", recvbuf, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val, _op_val(opx, recvbuf))
+    _call("Allreduce", recvbuf, comm, _ptr(sendbuf), _ptr(recvbuf), _cint(count), T.val, _op_val(opx, recvbuf))
     return recvbuf
 
 
@@ -1075,7 +1075,7 @@ def _scan_common(args, exclusive):
     sendbuf, recvbuf, count, op, comm = _scan_dispatch(args)
     T = _eltype(recvbuf)
     opx = _as_op(op, _dtype(recvbuf))
-    _call("Exscan" if exclusive else "Scan", recvbuf, comm, _ptr(sendbuf), _ptr(recvbuf), int(count), T.val,
+    _call("Exscan" if exclusive else "Scan", recvbuf, comm, _ptr(sendbuf), _ptr(recvbuf), _cint(count), T.val,
           _op_val(opx, recvbuf))
     return recvbuf
 
@@ -1117,7 +1117,7 @@ def Reduce_local_(inbuf, inoutbuf, count, op):
     """MPI_Reduce_local (mpi.h:1357): inoutbuf = op(inoutbuf, inbuf)."""
     T = _eltype(inoutbuf)
     opx = _as_op(op, _dtype(inoutbuf))
-    _check(lib().mpigx_reduce_local(_ptr(inbuf), _ptr(inoutbuf), int(count), T.val, opx.val))
+    _check(lib().mpigx_reduce_local(_ptr(inbuf), _ptr(inoutbuf), _cint(count), T.val, opx.val))
     return inoutbuf
 
 
