@@ -14,7 +14,8 @@ which stays.  Each worker reports the protocol it actually ran
 (`mpigx_comm_diag_peer_mem`) and these tests check it before the parity
 results: the MPICH golden fixtures (staged, LL and zero-copy paths), the
 headline sizes on whole buffers, the MPICH large-count fixtures and the
-zero-copy view protocol.
+zero-copy view protocol — at n = 8 too, the rank count of the driver's
+8-GPU node.
 
 The reference call behind all of it is MPI.Allreduce! and friends,
 /root/reference/src/collective.jl:698-700 (and :605-618, :29-37, :295-307,
@@ -50,7 +51,7 @@ def _check_protocol(res, n):
         assert same == full, x
 
 
-@pytest.mark.parametrize("n", [2, 3, 4])
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_golden_collectives_xdev(n):
     """Every MPICH golden case (Allreduce / Reduce / Bcast / Allgather /
     Alltoall / Scan / Exscan / v-collectives, LL step and tuner cases)."""
@@ -61,7 +62,7 @@ def test_golden_collectives_xdev(n):
     assert all(x["nfail"] == 0 and x["checks"] > 200 for x in res), res
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_golden_collectives_zero_copy_xdev(n):
     """The zero-copy paths (pull, push, pull-push, ring, zero-copy Reduce /
     Scan / Bcast relay) at every fixture size."""
@@ -73,7 +74,7 @@ def test_golden_collectives_zero_copy_xdev(n):
     assert all(x["nfail"] == 0 and x["checks"] > 200 for x in res), res
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_headline_sizes_xdev(n):
     """256 MiB Allreduce (whole buffer), 512 MiB Bcast / Allgather /
     Alltoall, 64 Mi-element Scan / Exscan / Reduce, every algorithm at 16 MiB
