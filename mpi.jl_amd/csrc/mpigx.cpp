@@ -29,6 +29,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mpigx_diag.h"
@@ -304,6 +305,40 @@ int shared_gate(mpigx_comm* c) {
   return host_allgather_wait(c, &z, sizeof z, all, true);
 }
 
+// Stream-ordered (RCCL-style) launches wait for a late peer too (round 5):
+// like ncclAllReduce they have no time limit — nobody waits on the host for
+// them — and this thread, started with the communicator's first
+// stream-ordered launch, does what finish() does for a blocking call: it
+// publishes the launch this rank's GPU has reached (ShmRank.kseq_run) and
+// stores the cancel word when the wait cannot end, i.e. when a peer's
+// communicator failed or its process is gone (checked every 0.25 s).  The
+// cancelled kernels record a timeout in the error word, which the next
+// synchronizing call reports (mpigx_comm_synchronize / any blocking call),
+// breaking the communicator.  Unlike a blocking call there is no stall
+// detection: a stream-ordered launch that never completes for a protocol
+// reason hangs, as an RCCL kernel would.
+void watch_peers(mpigx_comm* c) {
+  unsigned tick = 0;
+  while (!c->watcher_stop.load(std::memory_order_acquire)) {
+    usleep(10000);
+    if (!c->shm) continue;
+    c->shm->ranks[c->rank].kseq_run.store(*c->started, std::memory_order_release);
+    if (__atomic_load_n(c->cancel, __ATOMIC_ACQUIRE)) continue;  // already cancelled (finish or here)
+    if (++tick % 25) continue;
+    int who = peer_broken(c);
+    const char* why = who >= 0 ? "its communicator failed" : nullptr;
+    for (int q = 0; !why && q < c->n; ++q)
+      if (q != c->rank && peer_gone(c, q)) {
+        who = q;
+        why = "its process is gone";
+      }
+    if (why) {
+      fprintf(stderr, "[mpigx] rank %d: cancelling stream-ordered waits: rank %d: %s\n", c->rank, who, why);
+      __atomic_store_n(c->cancel, 1u, __ATOMIC_RELEASE);
+    }
+  }
+}
+
 PeerView make_view(mpigx_comm* c) {
   if (c->diag_trace) {  // before every launch: the peers' canaries through my mappings of their signal arrays
     for (int q = 0; q < c->n; ++q) {
@@ -340,10 +375,11 @@ PeerView make_view(mpigx_comm* c) {
   pv.seq = c->launch_seq + 1;
   pv.kseq = c->kseq + 1;
   pv.started = c->started_dev;
-  // blocking calls completed through the completion word have a host that
-  // watches the peers while it waits (finish): their polls wait for a late
-  // peer until that host cancels; stream-ordered ones keep the timeout
-  pv.cancel = pv.done ? c->cancel_dev : nullptr;
+  // every launch waits for a late peer until its host cancels: a blocking
+  // call's host watches the peers while it waits (finish), a stream-ordered
+  // launch's peers are watched by watch_peers (started here, once)
+  pv.cancel = c->cancel_dev;
+  if (!pv.done && c->n > 1 && c->shm && !c->watcher) c->watcher = new std::thread(watch_peers, c);
   pv.stamps = c->stamps;
   // each peer gets its words in the array of ITS memory type for me: ordinary
   // memory between ranks of one device, uncached across devices (one memory
@@ -2131,6 +2167,12 @@ int knobs_from_env(mpigx_comm* c) {
 void comm_release(mpigx_comm* c) {
   (void)hipSetDevice(c->device);
   if (c->stream || c->launch_seq) (void)hipStreamSynchronize(c->stream);
+  if (c->watcher) {  // after the drain: a waiting stream-ordered launch needs it to be cancelled
+    c->watcher_stop.store(true, std::memory_order_release);
+    c->watcher->join();
+    delete c->watcher;
+    c->watcher = nullptr;
+  }
   rt::rma_destroy(c);
   rt::p2p_destroy(c);
   for (int q = 0; q < c->n; ++q) {

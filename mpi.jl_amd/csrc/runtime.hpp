@@ -6,6 +6,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -284,6 +285,10 @@ struct mpigx_comm {
   // tools/ipc_torch.py); MPIGX_IPC_ALLOC_MAX overrides (tests).
   long long ipc_alloc_max = 0;
   int hip_runtime = 0;                  // hipRuntimeGetVersion of the runtime this process loaded
+  // Stream-ordered launches' peer watcher (mpigx.cpp watch_peers): started
+  // with the first stream-ordered launch, stopped in comm_release.
+  std::thread* watcher = nullptr;
+  std::atomic<bool> watcher_stop{false};
   std::mutex mu;
 };
 

@@ -16,6 +16,14 @@ watch the peers (mpigx.cpp finish, PeerView.cancel).
 * late_so — the same on a stream-ordered communicator with fresh 16 MiB
   buffers (a stream-ordered zero-copy call agrees on the view over the host
   control plane before its launch);
+* late_so_small — stream-ordered (RCCL-style): the early ranks' 4 KiB
+  Allreduce KERNELS are already waiting on the device (no host exchange at
+  this size) while the last rank sleeps; stream-ordered launches have no
+  time limit either, so the synchronize after them returns exact results
+  once the late rank arrives;
+* gone_so — stream-ordered, the last rank exits: the early ranks' waiting
+  kernels are cancelled by their peer watcher (mpigx.cpp watch_peers) and
+  the synchronize fails within seconds;
 * gone — after one good call the last rank exits without finalizing; the
   others' next Allreduce must fail (MPIError) within seconds instead of
   waiting for ever.
@@ -101,6 +109,48 @@ def main():
             fails.append("call after")
         MPI.Barrier(comm)
         MPI.Finalize()
+    elif scenario == "late_so_small":
+        L = MPI.lib()
+        small, sres = send[:1024].clone(), torch.full((1024,), -1.0, device="cuda")
+        MPI.api._check(L.mpigx_comm_set_blocking(comm.val, 0))
+        if r == n - 1:
+            time.sleep(2.5 * timeout_s)
+        t0 = time.time()
+        MPI.Allreduce_(small, sres, MPI.SUM, comm)
+        MPI.api._check(L.mpigx_comm_synchronize(comm.val))
+        torch.cuda.synchronize()
+        out["late_call_s"] = round(time.time() - t0, 3)
+        if not bool((sres == want).all()):
+            fails.append("late stream-ordered kernel")
+        MPI.api._check(L.mpigx_comm_set_blocking(comm.val, 1))
+        recv.fill_(-1)
+        MPI.Allreduce_(send, recv, MPI.SUM, comm)
+        if not bool((recv == want).all()):
+            fails.append("call after")
+        MPI.Barrier(comm)
+        MPI.Finalize()
+    elif scenario == "gone_so":
+        L = MPI.lib()
+        if r == n - 1:
+            sys.stdout.flush()
+            os._exit(0)
+        small, sres = send[:1024].clone(), torch.full((1024,), -1.0, device="cuda")
+        MPI.api._check(L.mpigx_comm_set_blocking(comm.val, 0))
+        t0 = time.time()
+        rc = 0
+        try:
+            MPI.Allreduce_(small, sres, MPI.SUM, comm)
+            rc = L.mpigx_comm_synchronize(comm.val)
+        except MPI.MPIError as e:
+            out["error"] = str(e)
+            rc = -1
+        if rc == 0:
+            fails.append("no error with a vanished peer (stream-ordered)")
+        out["gone_call_s"] = round(time.time() - t0, 3)
+        torch.cuda.synchronize()
+        out["fails"] = fails
+        print(json.dumps(out), flush=True)
+        os._exit(1 if fails else 0)
     elif scenario == "broken":
         if r == n - 1:
             MPI.lib().mpigx_comm_diag_break(comm.val)
