@@ -2224,6 +2224,13 @@ int comm_init(mpigx_comm* c, const IdPayload& p, bool* shm_created) {
   c->ipc_alloc_max = c->hip_runtime < 70200000 ? (1ll << 31) - 1 : 0;
   c->ipc_alloc_max = env_ll("MPIGX_IPC_ALLOC_MAX", c->ipc_alloc_max);
 
+  if (c->ipc_alloc_max > 0 && (long long)c->stage_bytes > c->ipc_alloc_max) {
+    // every peer maps the arena: one the loaded runtime cannot IPC-map would
+    // hang the rendezvous (runtime.hpp ipc_alloc_max)
+    fprintf(stderr, "[mpigx] MPIGX_STAGING_BYTES=%zu exceeds what HIP runtime %d can IPC-map (%lld bytes)\n",
+            (size_t)c->stage_bytes, c->hip_runtime, c->ipc_alloc_max);
+    return MPIGX_ERR_ARG;
+  }
   HIPCK(hipMalloc(&c->stage, c->stage_bytes));
   // rows [0, kMaxBlocks): per-block barriers; row kMaxBlocks: whole-launch
   // barrier (device.hpp rank_barrier_grid)
