@@ -35,10 +35,18 @@ IN_PLACE = ctypes.c_void_p(-1 & ((1 << 64) - 1))
 AR_ALGOS = ("ll", "ll2", "oneshot", "twoshot") + (("push", "pull_generic", "pullpush") if os.environ.get("MPIGX_ZC_MIN") else ())
 
 
+# device buffers made for the current call: P(dev(x)) hands out a raw
+# pointer, so the tensor must outlive the call (a freed block goes back to
+# torch's cache, and the next allocation may take it before the engine reads
+# it); Runner.run clears the list when the next call starts
+_KEEP = []
+
+
 def dev(a):
     raw = np.frombuffer(np.ascontiguousarray(a).tobytes(), dtype=np.uint8)
     t = torch.empty(max(raw.size, 1) + 64, dtype=torch.uint8, device="cuda")[: raw.size]
     t.copy_(torch.from_numpy(raw.copy()))
+    _KEEP.append(t)
     return t
 
 
@@ -71,6 +79,7 @@ class Runner:
     def run(self, coll, ins, dtname, opname, count, root=0, inplace=False):
         """Run one collective on my input ins[r]; return my output (numpy) or None."""
         L, r, n, cv = self.L, self.r, self.n, self.comm.val
+        _KEEP.clear()
         npdt = M.DTYPES[dtname][1]
         h = M.DTYPES[dtname][0]
         op = M.OPS.get(opname, 0) if opname else 0
