@@ -80,6 +80,130 @@ def dev_at(a, off_elems):
     return t
 
 
+def vcoll_cases(comm, seed, ncases):
+    """Gatherv / Scatterv / Allgatherv / Alltoallv (collective.jl:363-382,
+    :156-175, :424-442, :545-559) with random per-rank counts (zeros
+    included) and displacements with gaps between the blocks: the bytes in
+    the gaps and past the last block must stay untouched."""
+    r, n = MPI.Comm_rank(comm), MPI.Comm_size(comm)
+    L, cv = MPI.lib(), comm.val
+    I = ctypes.c_int * 16
+    rng = np.random.default_rng(seed + 7919)
+    fails, ran = [], 0
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    for k in range(ncases):
+        coll = ("gatherv", "scatterv", "allgatherv", "alltoallv")[k % 4]
+        dt = TYPES[rng.integers(len(TYPES))]
+        npdt = M.DTYPES[dt][1]
+        h = M.DTYPES[dt][0]
+        es = np.dtype(npdt).itemsize
+        big = rng.integers(3) == 0
+        hi = int(rng.integers(1, (256 << 10) // es if big else 3000))
+        C = rng.integers(0, hi, size=(n, n))
+        C[rng.random((n, n)) < 0.2] = 0  # some empty blocks
+        gaps = rng.integers(0, 4, size=(n, n))
+        root = int(rng.integers(n))
+        cseed = int(rng.integers(1 << 30))
+
+        def displs(counts, g):
+            d, acc = [], 0
+            for c_, g_ in zip(counts, g):
+                acc += int(g_)
+                d.append(acc)
+                acc += int(c_)
+            return d, acc + 8  # 8 spare elements at the end
+
+        def layout(counts, g, blocks):
+            """sentinel-filled buffer with blocks[p] at displs[p]"""
+            d, tot = displs(counts, g)
+            buf = np.frombuffer(np.full(tot * es, 0xCD, np.uint8).tobytes(), dtype=npdt).copy()
+            for p, b in enumerate(blocks):
+                if b is not None:
+                    buf[d[p]:d[p] + counts[p]] = b
+            return buf, d
+
+        srcs = make(dt, "SUM", n, int(C.sum()) + 1, cseed)  # rank p's data
+        if coll in ("gatherv", "allgatherv"):
+            cnt = [int(C[p][0]) for p in range(n)]
+            mine = srcs[r][:cnt[r]]
+            exp, d = layout(cnt, gaps[0], [srcs[p][:cnt[p]] for p in range(n)])
+            init, _ = layout(cnt, gaps[0], [None] * n)
+            recv = dev_at(init, 0)
+            sb = dev_at(mine, int(rng.integers(3)))
+            if coll == "gatherv":
+                rc = L.mpigx_gatherv(P(sb), cnt[r], h, P(recv) if r == root else None, I(*cnt), I(*d), h, root, cv)
+                want = exp if r == root else None
+            else:
+                rc = L.mpigx_allgatherv(P(sb), cnt[r], h, P(recv), I(*cnt), I(*d), h, cv)
+                want = exp
+        elif coll == "scatterv":
+            cnt = [int(C[0][p]) for p in range(n)]
+            o = [sum(cnt[:p]) for p in range(n)]  # block p = the root's elements o[p] .. o[p] + cnt[p]
+            sendbuf, d = layout(cnt, gaps[0], [srcs[root][o[p]:o[p] + cnt[p]] for p in range(n)])
+            sb = dev_at(sendbuf, 0) if r == root else None
+            want = np.concatenate([srcs[root][o[r]:o[r] + cnt[r]],
+                                   np.frombuffer(np.full(8 * es, 0xCD, np.uint8).tobytes(), dtype=npdt)])
+            recv = dev_at(np.frombuffer(np.full((cnt[r] + 8) * es, 0xCD, np.uint8).tobytes(), dtype=npdt).copy(),
+                          int(rng.integers(3)))
+            rc = L.mpigx_scatterv(P(sb) if sb is not None else None, I(*cnt), I(*d), h, P(recv), cnt[r], h, root, cv)
+        else:  # alltoallv: rank p sends C[p][q] elements to q
+            sc = [int(C[r][q]) for q in range(n)]
+            rcn = [int(C[p][r]) for p in range(n)]
+            def block(p, q):  # what rank p sends rank q: its elements sum(C[p][:q]) ..
+                o_ = int(C[p][:q].sum())
+                return srcs[p][o_:o_ + int(C[p][q])]
+
+            sendbuf, sd = layout(sc, gaps[r], [block(r, q) for q in range(n)])
+            exp, rd = layout(rcn, gaps[(r + 1) % n], [block(p, r) for p in range(n)])
+            init, _ = layout(rcn, gaps[(r + 1) % n], [None] * n)
+            sb = dev_at(sendbuf, int(rng.integers(3)))
+            recv = dev_at(init, 0)
+            rc = L.mpigx_alltoallv(P(sb), I(*sc), I(*sd), h, P(recv), I(*rcn), I(*rd), h, cv)
+            want = exp
+        ran += 1
+        if rc != 0:
+            fails.append({"coll": coll, "k": k, "dtype": dt, "rc": int(rc)})
+            continue
+        if want is not None:
+            got = recv.cpu().numpy().view(np.uint8)
+            if not np.array_equal(got, np.ascontiguousarray(want).view(np.uint8)):
+                fails.append({"coll": coll, "k": k, "dtype": dt, "counts": C.tolist()[:2], "root": root})
+    return fails, ran
+
+
+def local_cases(seed, ncases):
+    """The local MPI.Op kernel (config 2's API, mpigx_reduce_local_multi):
+    2-16 inputs, every valid (op, type), odd counts and unaligned buffers,
+    against the oracle's fold of the same inputs (an nin-rank Allreduce)."""
+    rng = np.random.default_rng(seed + 104729)
+    fails, ran = [], 0
+    stream = torch.cuda.current_stream()
+    while ran < ncases:
+        dt = TYPES[rng.integers(len(TYPES))]
+        op = list(M.OPS)[rng.integers(len(M.OPS))]
+        if M.op_valid(dt, op) != 0:
+            continue
+        nin = int(rng.integers(2, 17))
+        es = np.dtype(M.DTYPES[dt][1]).itemsize
+        count = int(rng.integers(1, (4 << 20) // es if rng.integers(3) == 0 else 5000))
+        ins = make(dt, op, nin, count, int(rng.integers(1 << 30)), edge=bool(rng.integers(3) == 0))
+        dins = [dev_at(x, int(rng.integers(3))) for x in ins]
+        out = dev_at(np.zeros_like(ins[0]), int(rng.integers(3)))
+        arr = (ctypes.c_void_p * nin)(*[t.data_ptr() for t in dins])
+        rc = MPI.lib().mpigx_reduce_local_multi(arr, nin, ctypes.c_void_p(out.data_ptr()), count, M.DTYPES[dt][0],
+                                                M.OPS[op], 0, ctypes.c_void_p(stream.cuda_stream))
+        torch.cuda.synchronize()
+        ran += 1
+        if rc != 0:
+            fails.append({"coll": "reduce_local_multi", "dtype": dt, "op": op, "nin": nin, "rc": int(rc)})
+            continue
+        exp = M.allreduce(ins, dt, op)[0]
+        got = out.cpu().numpy().view(M.DTYPES[dt][1])
+        if not same_bits(got, exp, bf16=(dt == "BFLOAT16")):
+            fails.append({"coll": "reduce_local_multi", "dtype": dt, "op": op, "nin": nin, "count": count})
+    return fails, ran
+
+
 def main():
     comm = MPI.Init()
     r, n = MPI.Comm_rank(comm), MPI.Comm_size(comm)
@@ -170,6 +294,13 @@ def main():
             bad = np.nonzero(diff)[0]
             fails.append(dict(desc, first_bad=int(bad[0]) if bad.size else -1, nbad=int(bad.size)))
     MPI.set_knob(comm, "ALGO", None)
+    f2, r2 = vcoll_cases(comm, int(os.environ.get("FUZZ_SEED", 1)), int(os.environ.get("FUZZ_VCASES", 40)))
+    fails += f2
+    ran += r2
+    if r == 0:
+        f3, r3 = local_cases(int(os.environ.get("FUZZ_SEED", 1)), int(os.environ.get("FUZZ_LCASES", 40)))
+        fails += f3
+        ran += r3
     MPI.Barrier(comm)
     MPI.Finalize()
     print(json.dumps({"rank": r, "n": n, "nfail": len(fails), "ran": ran, "fails": fails[:6]}), flush=True)

@@ -1,8 +1,11 @@
 """Randomized parity sweep (tests/spmd/fuzz_worker.py): seeded random
 collectives — every valid (op, type) pair, counts across the LL / one-shot /
 two-shot / zero-copy thresholds, unaligned buffers, IN_PLACE, every root,
-every Allreduce algorithm — against the MPICH-pinned oracle, bit for bit
-(any NaN = any NaN).  The zero-copy threshold is lowered to 1 MiB so the
+every Allreduce algorithm — plus Gatherv / Scatterv / Allgatherv /
+Alltoallv with random counts (zeros included) and gapped displacements
+(the gaps must stay untouched) and the local MPI.Op kernel over 2-16
+unaligned inputs, against the MPICH-pinned oracle, bit for bit (any NaN =
+any NaN).  The zero-copy threshold is lowered to 1 MiB so the
 zero-copy kernels see odd counts and unaligned buffers too.  Run with the
 same-GPU protocol and, at n = 3 and 8, with the cross-GPU one
 (MPIGX_PEER_MEM=xdev, no host gate)."""
