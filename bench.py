@@ -484,6 +484,23 @@ def bench_allreduce(args):
                 tw, _ = time_ar(nb, 20, 5)
                 sweep[f"{nb >> 10}KiB_{algo}_us"] = round(tw * 1e6, 2)
             MPI.set_knob(comm, "ALGO", None)
+        # the engine's own per-call latency on the default path: K back-to-back
+        # calls through the raw C ABI (what MPI.jl's ccall makes), no events and
+        # no Python mirror in the loop, max over ranks
+        for nb in (8, 8 << 10, 64 << 10):
+            cnt = max(1, nb // 4)
+            xs, xr = rank_input(rank, cnt), torch.empty(cnt, device=dev)
+            ps, pr = ctypes.c_void_p(xs.data_ptr()), ctypes.c_void_p(xr.data_ptr())
+            Lr, fl, sm, cvv = MPI.lib(), MPI.FLOAT.val, MPI.SUM.val, comm.val
+            for _ in range(30):
+                Lr.mpigx_allreduce(ps, pr, cnt, fl, sm, cvv)
+            dist.barrier()
+            reps = 300
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                Lr.mpigx_allreduce(ps, pr, cnt, fl, sm, cvv)
+            (tw,) = tmax((time.perf_counter() - t0) / reps)
+            sweep[f"{nb >> 10}KiB_raw_abi_us" if nb >= 1024 else f"{nb}B_raw_abi_us"] = round(tw * 1e6, 2)
         rings = len(M.ring_strides(n, 4))
         for algo, chans in (("pull", 1), ("pull_generic", 1), ("push", 1), ("pullpush", 1), ("ring", 1),
                             ("ring", rings)):
