@@ -11,10 +11,14 @@ from spmd_launch import ROOT, launch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n", [2, 4])
-def test_reference_suite_device(n):
+@pytest.mark.parametrize("n,cfg", [(2, "same"), (4, "same"), (3, "xdev"), (8, "xdev")])
+def test_reference_suite_device(n, cfg):
+    """cfg xdev: the one-rank-per-GPU signalling (MPIGX_PEER_MEM=xdev, no host
+    gate; tests/test_xdev_gpu.py), at n = 8 the driver node's rank count."""
     env = {"MPIGX_TEST_ARRAYTYPE": "ROCArray", "MPIGX_DEVICE": "0", "MPIGX_MAX_BLOCKS": "16",
            "MPIGX_TIMEOUT_MS": "30000", "MPIGX_STAGING_BYTES": str(16 << 20)}
+    if cfg == "xdev":
+        env.update(MPIGX_PEER_MEM="xdev", MPIGX_SHARED_GATE="0")
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "ref_tests.py"), n, timeout=600, extra_env=env)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
     assert all(rc == 0 for rc in rcs), "\n".join(o[-2000:] for o in outs)
