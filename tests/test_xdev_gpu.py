@@ -107,3 +107,24 @@ def test_zero_copy_views_xdev():
     assert len(res) == 2, msg
     _check_protocol(res, 2)
     assert all(x["nfail"] == 0 for x in res), res
+
+
+@pytest.mark.parametrize("worker", ["headline_worker.py", "golden_worker.py"])
+def test_production_grid_xdev(worker):
+    """Two ranks, the cross-GPU signalling AND the production grid: without
+    the shared-GPU residency headroom (MPIGX_SHARE_HEADROOM=0) every
+    collective kernel of a 2-rank communicator gets 256 blocks, as on a GPU of
+    its own (bench r05p: pull / push / pull-push phases report 256 blocks),
+    so the per-block barrier slots of blocks 128-255 run the uncached
+    protocol too.  Headline sizes on whole buffers; the MPICH fixtures through
+    the zero-copy paths."""
+    env = dict(XDEV, MPIGX_SHARE_HEADROOM="0")
+    if worker == "headline_worker.py":
+        env["MPIGX_HEADLINE_EXTRA"] = "1"
+    else:
+        env.update(MPIGX_ZC_MIN="1", MPIGX_ZC_REQUIRE="1", MPIGX_STAGING_BYTES=str(64 << 20))
+    rcs, res, msg = _run(worker, 2, env)
+    assert all(rc == 0 for rc in rcs), msg
+    assert len(res) == 2, msg
+    _check_protocol(res, 2)
+    assert all(x["nfail"] == 0 for x in res), res
