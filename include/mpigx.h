@@ -107,6 +107,17 @@ typedef struct {
 int mpigx_get_version(int *major, int *minor);
 /* MPI_Error_string analogue (src/error.jl:11-19). `len` in/out like MPI. */
 int mpigx_error_string(int errorcode, char *string, int *resultlen);
+/* Thread level the engine provides (environment.jl:111-162 Init_thread /
+ * Query_thread; MPICH values THREAD_SINGLE 0 .. THREAD_MULTIPLE 3): 3.
+ * Point-to-point and RMA calls may come from any thread at once (one
+ * process-wide lock; blocking p2p calls release it between polls, as in
+ * test/test_threads.jl's threaded Isend / Irecv); collectives: one call at a
+ * time per communicator, as MPI requires.  Needs no GPU. */
+#define MPIGX_THREAD_SINGLE 0
+#define MPIGX_THREAD_FUNNELED 1
+#define MPIGX_THREAD_SERIALIZED 2
+#define MPIGX_THREAD_MULTIPLE 3
+int mpigx_query_thread(int *provided);
 /* Host-only validation of (datatype, op): MPIGX_SUCCESS, MPIGX_ERR_TYPE or
  * MPIGX_ERR_OP following MPICH's op x type matrix.  Needs no GPU. */
 int mpigx_op_valid(int datatype, int op);

@@ -1857,7 +1857,19 @@ int acc_check(int datatype, int op, int* rep, int* esize, int* oc) {
   *oc = o;
   return MPIGX_SUCCESS;
 }
+bool peer_dead(const mpigx_comm* c) {
+  if (!c || !c->shm || c->n <= 1) return false;
+  if (peer_broken(c) >= 0) return true;
+  for (int q = 0; q < c->n; ++q)
+    if (q != c->rank && peer_gone(c, q)) return true;
+  return false;
+}
+std::recursive_mutex& big_lock() {
+  static std::recursive_mutex m;
+  return m;
+}
 void progress_all(mpigx_comm* c) {
+  std::lock_guard<std::recursive_mutex> g(big_lock());
   if (c->in_progress) return;
   c->in_progress = true;
   if (c->p2p) p2p_progress(c);
@@ -1883,6 +1895,11 @@ int mpigx_get_version(int* major, int* minor) {
   return MPIGX_SUCCESS;
 }
 
+int mpigx_query_thread(int* provided) {
+  if (!provided) return MPIGX_ERR_ARG;
+  *provided = MPIGX_THREAD_MULTIPLE;  // rt::big_lock (runtime.hpp)
+  return MPIGX_SUCCESS;
+}
 int mpigx_error_string(int code, char* str, int* len) {
   const char* s;
   switch (code) {

@@ -480,11 +480,38 @@ void progress_reqs(int count, const mpigx_request_t* reqs) {
 
 // Waiting: MPI waits forever; a dead peer would hang the caller, so waits give
 // up after the communicator's timeout (MPIGX_TIMEOUT_MS) with MPI_ERR_OTHER.
+// How long a blocking point-to-point call waits (round 5): as long as its
+// peers live, as MPI's Wait / Recv do (pointtopoint.jl) — the same rule as
+// the collectives' late-rank waits.  It gives up only when a peer of one of
+// its communicators is gone or its communicator failed (rt::peer_dead,
+// checked every 0.25 s); past MPIGX_TIMEOUT_MS it says once on stderr that it
+// is still waiting.
 struct Deadline {
-  double t0, lim;
+  static constexpr int kMax = 4;
+  mpigx_comm* comms[kMax] = {};
+  int nc = 0;
+  double t0, lim, next;
   unsigned spins = 0;
-  explicit Deadline(double l) : t0(rt::wall()), lim(l) {}
-  bool expired() { return (++spins & 1023) == 0 && rt::wall() - t0 > lim; }
+  bool noted = false;
+  explicit Deadline(double l) : t0(rt::wall()), lim(l), next(t0 + 0.25) {}
+  void add(mpigx_comm* c) {
+    for (int i = 0; i < nc; ++i)
+      if (comms[i] == c) return;
+    if (c && nc < kMax) comms[nc++] = c;
+  }
+  bool expired() {
+    if ((++spins & 1023) != 0) return false;
+    const double t = rt::wall();
+    if (t < next) return false;
+    next = t + 0.25;
+    for (int i = 0; i < nc; ++i)
+      if (rt::peer_dead(comms[i])) return true;
+    if (!noted && t - t0 > lim) {
+      noted = true;
+      fprintf(stderr, "mpigx: a point-to-point wait has lasted %.0f s; still waiting for the peer\n", t - t0);
+    }
+    return false;
+  }
 };
 
 double limit_of(int count, const mpigx_request_t* reqs) {
@@ -492,6 +519,11 @@ double limit_of(int count, const mpigx_request_t* reqs) {
   for (int i = 0; i < count; ++i)
     if (Req* r = lookup(reqs[i])) l = std::max(l, limit_s(r->c));
   return l;
+}
+// the communicators of a request set, for Deadline (caller holds big_lock)
+void comms_of(Deadline& d, int count, const mpigx_request_t* reqs) {
+  for (int i = 0; i < count; ++i)
+    if (Req* r = lookup(reqs[i])) d.add(r->c);
 }
 
 int validate_reqs(int count, const mpigx_request_t* reqs) {
@@ -544,6 +576,7 @@ extern "C" {
 
 int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpigx_comm_t c,
                 mpigx_request_t* request) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request) return MPIGX_ERR_ARG;
   rt::TypeDesc td;
   int rc = check_common(c, buf, count, datatype, &td);
@@ -614,6 +647,7 @@ int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpi
 
 int mpigx_irecv(void* buf, int count, int datatype, int source, int tag, mpigx_comm_t c,
                 mpigx_request_t* request) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request) return MPIGX_ERR_ARG;
   rt::TypeDesc td;
   int rc = check_common(c, buf, count, datatype, &td);
@@ -671,6 +705,7 @@ int mpigx_irecv(void* buf, int count, int datatype, int source, int tag, mpigx_c
 }
 
 int mpigx_test(mpigx_request_t* request, int* flag, mpigx_status_t* status) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request || !flag) return MPIGX_ERR_ARG;
   if (*request == MPIGX_REQUEST_NULL) {
     *flag = 1;
@@ -693,8 +728,17 @@ int mpigx_test(mpigx_request_t* request, int* flag, mpigx_status_t* status) {
 
 int mpigx_wait(mpigx_request_t* request, mpigx_status_t* status) {
   if (!request) return MPIGX_ERR_ARG;
-  if (*request != MPIGX_REQUEST_NULL && !lookup(*request)) return MPIGX_ERR_REQUEST;
-  Deadline dl(limit_of(1, request));
+  double lim;
+  {  // the request table under the lock; the wait itself polls without it
+    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    if (*request != MPIGX_REQUEST_NULL && !lookup(*request)) return MPIGX_ERR_REQUEST;
+    lim = limit_of(1, request);
+  }
+  Deadline dl(lim);
+  {
+    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    comms_of(dl, 1, request);
+  }
   for (;;) {
     int flag = 0;
     const int rc = mpigx_test(request, &flag, status);
@@ -704,6 +748,7 @@ int mpigx_wait(mpigx_request_t* request, mpigx_status_t* status) {
 }
 
 int mpigx_testall(int count, mpigx_request_t* requests, int* flag, mpigx_status_t* statuses) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!flag) return MPIGX_ERR_ARG;
   int rc = validate_reqs(count, requests);
   if (rc) return rc;
@@ -734,9 +779,18 @@ int mpigx_testall(int count, mpigx_request_t* requests, int* flag, mpigx_status_
 }
 
 int mpigx_waitall(int count, mpigx_request_t* requests, mpigx_status_t* statuses) {
-  int rc = validate_reqs(count, requests);
-  if (rc) return rc;
-  Deadline dl(limit_of(count, requests));
+  int rc;
+  double lim;
+  {
+    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    if ((rc = validate_reqs(count, requests))) return rc;
+    lim = limit_of(count, requests);
+  }
+  Deadline dl(lim);
+  {
+    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    comms_of(dl, count, requests);
+  }
   for (;;) {
     int flag = 0;
     rc = mpigx_testall(count, requests, &flag, statuses);
@@ -746,6 +800,7 @@ int mpigx_waitall(int count, mpigx_request_t* requests, mpigx_status_t* statuses
 }
 
 int mpigx_testany(int count, mpigx_request_t* requests, int* index, int* flag, mpigx_status_t* status) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!index || !flag) return MPIGX_ERR_ARG;
   int rc = validate_reqs(count, requests);
   if (rc) return rc;
@@ -775,9 +830,18 @@ int mpigx_testany(int count, mpigx_request_t* requests, int* index, int* flag, m
 
 int mpigx_waitany(int count, mpigx_request_t* requests, int* index, mpigx_status_t* status) {
   if (!index) return MPIGX_ERR_ARG;
-  int rc = validate_reqs(count, requests);
-  if (rc) return rc;
-  Deadline dl(limit_of(count, requests));
+  int rc;
+  double lim;
+  {
+    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    if ((rc = validate_reqs(count, requests))) return rc;
+    lim = limit_of(count, requests);
+  }
+  Deadline dl(lim);
+  {
+    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    comms_of(dl, count, requests);
+  }
   for (;;) {
     int flag = 0;
     rc = mpigx_testany(count, requests, index, &flag, status);
@@ -788,6 +852,7 @@ int mpigx_waitany(int count, mpigx_request_t* requests, int* index, mpigx_status
 
 int mpigx_testsome(int incount, mpigx_request_t* requests, int* outcount, int* indices,
                    mpigx_status_t* statuses) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!outcount) return MPIGX_ERR_ARG;
   int rc = validate_reqs(incount, requests);
   if (rc) return rc;
@@ -817,9 +882,18 @@ int mpigx_testsome(int incount, mpigx_request_t* requests, int* outcount, int* i
 int mpigx_waitsome(int incount, mpigx_request_t* requests, int* outcount, int* indices,
                    mpigx_status_t* statuses) {
   if (!outcount) return MPIGX_ERR_ARG;
-  int rc = validate_reqs(incount, requests);
-  if (rc) return rc;
-  Deadline dl(limit_of(incount, requests));
+  int rc;
+  double lim;
+  {
+    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    if ((rc = validate_reqs(incount, requests))) return rc;
+    lim = limit_of(incount, requests);
+  }
+  Deadline dl(lim);
+  {
+    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    comms_of(dl, incount, requests);
+  }
   for (;;) {
     rc = mpigx_testsome(incount, requests, outcount, indices, statuses);
     if (*outcount != 0) return rc;
@@ -828,6 +902,7 @@ int mpigx_waitsome(int incount, mpigx_request_t* requests, int* outcount, int* i
 }
 
 int mpigx_cancel(mpigx_request_t* request) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request) return MPIGX_ERR_ARG;
   Req* r = lookup(*request);
   if (!r) return MPIGX_ERR_REQUEST;
@@ -858,6 +933,7 @@ int mpigx_cancel(mpigx_request_t* request) {
 }
 
 int mpigx_request_free(mpigx_request_t* request) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request) return MPIGX_ERR_ARG;
   Req* r = lookup(*request);
   if (!r) return MPIGX_ERR_REQUEST;
@@ -909,6 +985,7 @@ int mpigx_sendrecv(const void* sendbuf, int sendcount, int sendtype, int dest, i
 }
 
 int mpigx_iprobe(int source, int tag, mpigx_comm_t c, int* flag, mpigx_status_t* status) {
+  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = rt::comm_check(c);
   if (rc) return rc;
   if (!flag) return MPIGX_ERR_ARG;
@@ -941,6 +1018,7 @@ int mpigx_probe(int source, int tag, mpigx_comm_t c, mpigx_status_t* status) {
   int rc = rt::comm_check(c);
   if (rc) return rc;
   Deadline dl(limit_s(c));
+  dl.add(c);
   for (;;) {
     int flag = 0;
     rc = mpigx_iprobe(source, tag, c, &flag, status);

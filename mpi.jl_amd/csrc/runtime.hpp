@@ -306,6 +306,18 @@ void unpin(mpigx_comm* c, char* base);
 int host_allgather(mpigx_comm* c, const void* mine, int len, void* out);
 // every engine's progress (p2p + RMA target side); safe to call anywhere
 void progress_all(mpigx_comm* c);
+// MPI_THREAD_MULTIPLE (mpigx_query_thread): one process-wide recursive lock,
+// taken by every non-blocking point-to-point call, every RMA call and every
+// progress pass.  Blocking point-to-point calls (Wait*, Send, Recv, Probe)
+// loop over their non-blocking forms, so they release it between polls and a
+// thread blocked in Wait never holds up another thread's Isend.  Collectives
+// take it only for their progress passes (one call at a time per
+// communicator, as MPI requires).
+std::recursive_mutex& big_lock();
+// Some peer of c can no longer take part: its process is gone or its
+// communicator failed (shm flags).  Point-to-point and RMA waits use it as
+// their only way out: like the collectives they wait for a live late peer.
+bool peer_dead(const mpigx_comm* c);
 // RMA accumulate (datatype, op) check incl. REPLACE / NO_OP: rep, size, op code
 int acc_check(int datatype, int op, int* rep, int* esize, int* oc);
 double wall();

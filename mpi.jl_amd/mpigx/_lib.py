@@ -35,6 +35,7 @@ DEVICE_FN = ctypes.CFUNCTYPE(None, c_void_p, c_void_p, c_longlong, c_int, c_void
 PROTOTYPES = {
     "mpigx_get_version": (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "mpigx_error_string": (c_int, [c_int, ctypes.c_char_p, ctypes.POINTER(c_int)]),
+    "mpigx_query_thread": (c_int, [ctypes.POINTER(c_int)]),
     "mpigx_op_valid": (c_int, [c_int, c_int]),
     "mpigx_type_size": (c_int, [c_int, ctypes.POINTER(c_int)]),
     "mpigx_get_unique_id": (c_int, [ctypes.POINTER(UniqueId)]),

@@ -437,6 +437,40 @@ def Init(threadlevel=None):
     return COMM_WORLD
 
 
+# environment.jl:111-116 ThreadLevel (MPICH values)
+THREAD_SINGLE, THREAD_FUNNELED, THREAD_SERIALIZED, THREAD_MULTIPLE = 0, 1, 2, 3
+
+
+def Init_thread(required):
+    """environment.jl:142-162: Init, then the provided thread level — the
+    engine's (mpigx_query_thread: THREAD_MULTIPLE) and, under mpiexec, host
+    libmpi's, whichever is lower; a warning when it is below `required`."""
+    Init()
+    p = ctypes.c_int(THREAD_SINGLE)
+    if COMM_WORLD is not None and COMM_WORLD.val:
+        _check(lib().mpigx_query_thread(ctypes.byref(p)))
+    else:
+        p.value = THREAD_MULTIPLE
+    provided = min(p.value, hostmpi.query_thread()) if _state["host"] and hasattr(hostmpi, "query_thread") \
+        else p.value
+    if provided < required:
+        import warnings
+        warnings.warn(f"Thread level requested = {required}, provided = {provided}")
+    _state["thread"] = provided
+    return provided
+
+
+def Query_thread():
+    """environment.jl:174-180"""
+    return _state.get("thread", THREAD_SINGLE)
+
+
+def Is_thread_main():
+    """environment.jl:190-196: the thread that initialized MPI."""
+    import threading
+    return threading.current_thread() is threading.main_thread()
+
+
 def Initialized():
     return _state["init"]
 

@@ -24,6 +24,12 @@ watch the peers (mpigx.cpp finish, PeerView.cancel).
 * gone_so — stream-ordered, the last rank exits: the early ranks' waiting
   kernels are cancelled by their peer watcher (mpigx.cpp watch_peers) and
   the synchronize fails within seconds;
+* late_p2p — point-to-point: rank 0 posts a blocking Recv! from the last
+  rank, which sleeps 2.5 x MPIGX_TIMEOUT_MS before its Send (pointtopoint.jl
+  Recv! blocks until the message arrives): exact, no error;
+* gone_p2p — rank 0's Recv! from the last rank, which exits instead: the
+  Recv fails within seconds (the peer is gone), not after a timeout and not
+  never;
 * gone — after one good call the last rank exits without finalizing; the
   others' next Allreduce must fail (MPIError) within seconds instead of
   waiting for ever.
@@ -151,6 +157,38 @@ def main():
         out["fails"] = fails
         print(json.dumps(out), flush=True)
         os._exit(1 if fails else 0)
+    elif scenario in ("late_p2p", "gone_p2p"):
+        last = n - 1
+        msg = torch.full((4096,), float(r + 1), device="cuda")
+        box = torch.zeros(4096, device="cuda")
+        if r == last:
+            if scenario == "gone_p2p":
+                sys.stdout.flush()
+                os._exit(0)
+            time.sleep(2.5 * timeout_s)
+            MPI.Send(msg, 0, 77, comm)
+        elif r == 0:
+            t0 = time.time()
+            try:
+                MPI.Recv_(box, last, 77, comm)
+                if scenario == "gone_p2p":
+                    fails.append("no error with a vanished sender")
+                elif not bool((box == float(last + 1)).all()):
+                    fails.append("late message")
+            except MPI.MPIError as e:
+                out["error"] = str(e)
+                if scenario == "late_p2p":
+                    fails.append("error waiting for a late sender")
+            out["late_call_s" if scenario == "late_p2p" else "gone_call_s"] = round(time.time() - t0, 3)
+        if scenario == "gone_p2p":
+            out.setdefault("gone_call_s", 0.0)  # ranks other than the receiver wait for nothing
+            out["fails"] = fails
+            print(json.dumps(out), flush=True)
+            os._exit(1 if fails else 0)
+        if r != 0:
+            out["late_call_s"] = 999.0  # not the waiting rank
+        MPI.Barrier(comm)
+        MPI.Finalize()
     elif scenario == "broken":
         if r == n - 1:
             MPI.lib().mpigx_comm_diag_break(comm.val)

@@ -1,0 +1,81 @@
+"""test/test_threads.jl restated on the Python mirror, device mode: MPI
+initialized with THREAD_MULTIPLE, then every rank posts N Irecv! / Isend
+pairs of one-element device views from a pool of threads at once
+(`Threads.@threads for i = 1:N`, test_threads.jl:33-36) and waits for all of
+them on the main thread.  ctypes releases the GIL around each call, so the
+threads really are inside libmpigx together (rt::big_lock, runtime.hpp).
+Beyond the reference's N = 10: the same with 256 pairs, 8 threads and three
+rounds, and a thread that waits on its own receive while other threads keep
+posting.  Launched by tests/test_reference_suite_gpu.py."""
+import json
+import os
+import sys
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "mpi.jl_amd"))
+
+import torch  # noqa: E402
+
+import mpigx as MPI  # noqa: E402
+
+FAIL = []
+NCHECK = [0]
+
+
+def check(cond, what):
+    NCHECK[0] += 1
+    if not bool(cond):
+        FAIL.append(what)
+
+
+def exchange(comm, n_msgs, nthreads, tag0):
+    size, rank = MPI.Comm_size(comm), MPI.Comm_rank(comm)
+    dst, src = (rank + 1) % size, (rank - 1) % size
+    send_arr = torch.arange(1, n_msgs + 1, dtype=torch.float64, device="cuda") + 1000 * rank
+    recv_arr = torch.zeros(n_msgs, dtype=torch.float64, device="cuda")
+    reqs = [None] * (2 * n_msgs)
+
+    def work(i):
+        reqs[n_msgs + i] = MPI.Irecv_(recv_arr[i:i + 1], src, tag0 + i, comm)
+        reqs[i] = MPI.Isend(send_arr[i:i + 1], dst, tag0 + i, comm)
+
+    with ThreadPoolExecutor(max_workers=nthreads) as ex:
+        list(ex.map(work, range(n_msgs)))
+    MPI.Waitall_(reqs)
+    want = torch.arange(1, n_msgs + 1, dtype=torch.float64, device="cuda") + 1000 * src
+    return torch.equal(recv_arr, want)
+
+
+def main():
+    provided = MPI.Init_thread(MPI.THREAD_MULTIPLE)       # test_threads.jl:11
+    check(MPI.THREAD_SINGLE <= provided <= MPI.THREAD_MULTIPLE, "provided range")  # :13
+    check(MPI.Query_thread() == provided, "Query_thread")   # :14
+    check(MPI.Is_thread_main(), "Is_thread_main")           # :15
+    comm = MPI.COMM_WORLD
+    check(provided == MPI.THREAD_MULTIPLE, "engine provides THREAD_MULTIPLE")
+    if provided == MPI.THREAD_MULTIPLE:
+        check(exchange(comm, 10, 10, 0), "N = 10 threaded Isend / Irecv")  # :26-40
+        for rnd in range(3):
+            check(exchange(comm, 256, 8, 1000 + 300 * rnd), f"256 pairs, 8 threads, round {rnd}")
+        # a thread blocked in Wait must not hold up another thread's Isend
+        size, rank = MPI.Comm_size(comm), MPI.Comm_rank(comm)
+        dst, src = (rank + 1) % size, (rank - 1) % size
+        got = torch.zeros(4, dtype=torch.float64, device="cuda")
+        out = torch.full((4,), float(rank), dtype=torch.float64, device="cuda")
+        waiter = threading.Thread(target=lambda: MPI.Wait_(MPI.Irecv_(got, src, 9000, comm)))
+        waiter.start()
+        MPI.Wait_(MPI.Isend(out, dst, 9000, comm))
+        waiter.join(60)
+        check(not waiter.is_alive() and bool((got == float(src)).all()), "blocked waiter + concurrent Isend")
+    MPI.Barrier(comm)
+    MPI.Finalize()
+    print(json.dumps({"rank": MPI.Comm_rank(comm), "provided": provided, "checks": NCHECK[0],
+                      "failures": FAIL[:10], "nfail": len(FAIL)}), flush=True)
+    sys.exit(1 if FAIL else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,7 +31,8 @@ def _results(outs):
 @pytest.mark.parametrize("cfg,n,scenario", [("gate", 2, "late"), ("gate", 4, "late"), ("xdev", 2, "late"),
                                              ("xdev", 2, "late_small"), ("xdev", 3, "late"),
                                              ("xdev", 2, "late_vx"), ("xdev", 2, "late_so"),
-                                             ("xdev", 2, "late_so_small"), ("gate", 3, "late_so_small")])
+                                             ("xdev", 2, "late_so_small"), ("gate", 3, "late_so_small"),
+                                             ("xdev", 2, "late_p2p")])
 def test_late_rank_is_waited_for(cfg, n, scenario):
     rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=(scenario,))
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-2000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
@@ -42,7 +43,8 @@ def test_late_rank_is_waited_for(cfg, n, scenario):
     assert min(early) >= 2.0 * 2.0, res  # they waited past their 2 s timeout
 
 
-@pytest.mark.parametrize("cfg,scenario", [("gate", "gone"), ("xdev", "gone"), ("xdev", "gone_so")])
+@pytest.mark.parametrize("cfg,scenario", [("gate", "gone"), ("xdev", "gone"), ("xdev", "gone_so"),
+                                          ("xdev", "gone_p2p")])
 def test_vanished_rank_fails_the_call(cfg, scenario):
     n = 3
     rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=(scenario,))
