@@ -1704,7 +1704,10 @@ int host_allgather_wait(mpigx_comm* c, const void* mine, int len, void* out, boo
   for (int q = 0; q < c->n; ++q) {
     unsigned spins = 0;
     while (c->shm->ranks[q].xseq.load(std::memory_order_acquire) < k) {
-      if ((spins & 63) == 0) rt::progress_all(c);
+      if ((spins & 63) == 0) {
+        rt::progress_all(c);
+        rt::yield_big_lock();  // a Win_fence / Comm_split caller lets other threads' p2p through
+      }
       if ((++spins & 4095) == 0) {
         const double t = now_s();
         if (!until_gone && t - t0 > limit) {
@@ -1864,12 +1867,24 @@ bool peer_dead(const mpigx_comm* c) {
     if (q != c->rank && peer_gone(c, q)) return true;
   return false;
 }
-std::recursive_mutex& big_lock() {
-  static std::recursive_mutex m;
+BigLock& big_lock() {
+  static BigLock m;
   return m;
 }
+void yield_big_lock() {
+  BigLock& b = big_lock();
+  if (b.owner.load(std::memory_order_relaxed) != std::this_thread::get_id()) return;
+  const int d = b.depth;
+  b.depth = 0;
+  b.owner.store(std::thread::id(), std::memory_order_relaxed);
+  b.m.unlock();
+  sched_yield();
+  b.m.lock();
+  b.owner.store(std::this_thread::get_id(), std::memory_order_relaxed);
+  b.depth = d;
+}
 void progress_all(mpigx_comm* c) {
-  std::lock_guard<std::recursive_mutex> g(big_lock());
+  std::lock_guard<BigLock> g(big_lock());
   if (c->in_progress) return;
   c->in_progress = true;
   if (c->p2p) p2p_progress(c);

@@ -576,7 +576,7 @@ extern "C" {
 
 int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpigx_comm_t c,
                 mpigx_request_t* request) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request) return MPIGX_ERR_ARG;
   rt::TypeDesc td;
   int rc = check_common(c, buf, count, datatype, &td);
@@ -647,7 +647,7 @@ int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpi
 
 int mpigx_irecv(void* buf, int count, int datatype, int source, int tag, mpigx_comm_t c,
                 mpigx_request_t* request) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request) return MPIGX_ERR_ARG;
   rt::TypeDesc td;
   int rc = check_common(c, buf, count, datatype, &td);
@@ -705,7 +705,7 @@ int mpigx_irecv(void* buf, int count, int datatype, int source, int tag, mpigx_c
 }
 
 int mpigx_test(mpigx_request_t* request, int* flag, mpigx_status_t* status) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request || !flag) return MPIGX_ERR_ARG;
   if (*request == MPIGX_REQUEST_NULL) {
     *flag = 1;
@@ -730,13 +730,13 @@ int mpigx_wait(mpigx_request_t* request, mpigx_status_t* status) {
   if (!request) return MPIGX_ERR_ARG;
   double lim;
   {  // the request table under the lock; the wait itself polls without it
-    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    std::lock_guard<rt::BigLock> big(rt::big_lock());
     if (*request != MPIGX_REQUEST_NULL && !lookup(*request)) return MPIGX_ERR_REQUEST;
     lim = limit_of(1, request);
   }
   Deadline dl(lim);
   {
-    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    std::lock_guard<rt::BigLock> big(rt::big_lock());
     comms_of(dl, 1, request);
   }
   for (;;) {
@@ -748,7 +748,7 @@ int mpigx_wait(mpigx_request_t* request, mpigx_status_t* status) {
 }
 
 int mpigx_testall(int count, mpigx_request_t* requests, int* flag, mpigx_status_t* statuses) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!flag) return MPIGX_ERR_ARG;
   int rc = validate_reqs(count, requests);
   if (rc) return rc;
@@ -782,13 +782,13 @@ int mpigx_waitall(int count, mpigx_request_t* requests, mpigx_status_t* statuses
   int rc;
   double lim;
   {
-    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    std::lock_guard<rt::BigLock> big(rt::big_lock());
     if ((rc = validate_reqs(count, requests))) return rc;
     lim = limit_of(count, requests);
   }
   Deadline dl(lim);
   {
-    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    std::lock_guard<rt::BigLock> big(rt::big_lock());
     comms_of(dl, count, requests);
   }
   for (;;) {
@@ -800,7 +800,7 @@ int mpigx_waitall(int count, mpigx_request_t* requests, mpigx_status_t* statuses
 }
 
 int mpigx_testany(int count, mpigx_request_t* requests, int* index, int* flag, mpigx_status_t* status) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!index || !flag) return MPIGX_ERR_ARG;
   int rc = validate_reqs(count, requests);
   if (rc) return rc;
@@ -833,13 +833,13 @@ int mpigx_waitany(int count, mpigx_request_t* requests, int* index, mpigx_status
   int rc;
   double lim;
   {
-    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    std::lock_guard<rt::BigLock> big(rt::big_lock());
     if ((rc = validate_reqs(count, requests))) return rc;
     lim = limit_of(count, requests);
   }
   Deadline dl(lim);
   {
-    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    std::lock_guard<rt::BigLock> big(rt::big_lock());
     comms_of(dl, count, requests);
   }
   for (;;) {
@@ -852,7 +852,7 @@ int mpigx_waitany(int count, mpigx_request_t* requests, int* index, mpigx_status
 
 int mpigx_testsome(int incount, mpigx_request_t* requests, int* outcount, int* indices,
                    mpigx_status_t* statuses) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!outcount) return MPIGX_ERR_ARG;
   int rc = validate_reqs(incount, requests);
   if (rc) return rc;
@@ -885,13 +885,13 @@ int mpigx_waitsome(int incount, mpigx_request_t* requests, int* outcount, int* i
   int rc;
   double lim;
   {
-    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    std::lock_guard<rt::BigLock> big(rt::big_lock());
     if ((rc = validate_reqs(incount, requests))) return rc;
     lim = limit_of(incount, requests);
   }
   Deadline dl(lim);
   {
-    std::lock_guard<std::recursive_mutex> big(rt::big_lock());
+    std::lock_guard<rt::BigLock> big(rt::big_lock());
     comms_of(dl, incount, requests);
   }
   for (;;) {
@@ -902,7 +902,7 @@ int mpigx_waitsome(int incount, mpigx_request_t* requests, int* outcount, int* i
 }
 
 int mpigx_cancel(mpigx_request_t* request) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request) return MPIGX_ERR_ARG;
   Req* r = lookup(*request);
   if (!r) return MPIGX_ERR_REQUEST;
@@ -933,7 +933,7 @@ int mpigx_cancel(mpigx_request_t* request) {
 }
 
 int mpigx_request_free(mpigx_request_t* request) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!request) return MPIGX_ERR_ARG;
   Req* r = lookup(*request);
   if (!r) return MPIGX_ERR_REQUEST;
@@ -985,7 +985,7 @@ int mpigx_sendrecv(const void* sendbuf, int sendcount, int sendtype, int dest, i
 }
 
 int mpigx_iprobe(int source, int tag, mpigx_comm_t c, int* flag, mpigx_status_t* status) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = rt::comm_check(c);
   if (rc) return rc;
   if (!flag) return MPIGX_ERR_ARG;

@@ -273,6 +273,7 @@ void apply_incoming(mpigx_win* w) {
 // ---------------------------------------------------------------------------
 int spin_progress(mpigx_win* w, Deadline& d) {
   rt::progress_all(w->c);
+  rt::yield_big_lock();  // other threads' calls go on while this one waits
   if (d.expired()) {
     rt::comm_mark_broken(w->c);
     return MPIGX_ERR_OTHER;
@@ -632,20 +633,20 @@ void rma_destroy(mpigx_comm* c) {
 extern "C" {
 
 int mpigx_win_create(void* base, long long size, int disp_unit, mpigx_comm_t c, mpigx_win_t* win) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!win) return MPIGX_ERR_ARG;
   if (size > 0 && !base) return MPIGX_ERR_BASE;
   return win_setup(c, MPIGX_WIN_FLAVOR_CREATE, (char*)base, size, disp_unit, win);
 }
 
 int mpigx_win_create_dynamic(mpigx_comm_t c, mpigx_win_t* win) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!win) return MPIGX_ERR_ARG;
   return win_setup(c, MPIGX_WIN_FLAVOR_DYNAMIC, nullptr, 0, 1, win);
 }
 
 int mpigx_win_allocate_shared(long long size, int disp_unit, mpigx_comm_t c, void* baseptr, mpigx_win_t* win) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!win || !baseptr) return MPIGX_ERR_ARG;
   int rc = rt::comm_check(c);
   if (rc) return rc;
@@ -676,7 +677,7 @@ int mpigx_win_allocate_shared(long long size, int disp_unit, mpigx_comm_t c, voi
 }
 
 int mpigx_win_shared_query(mpigx_win_t w, int rank, long long* size, int* disp_unit, void* baseptr) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   if (w->flavor != MPIGX_WIN_FLAVOR_SHARED) return MPIGX_ERR_RMA_FLAVOR;
@@ -702,14 +703,14 @@ int mpigx_win_shared_query(mpigx_win_t w, int rank, long long* size, int* disp_u
 }
 
 int mpigx_win_get_flavor(mpigx_win_t w, int* flavor) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!w) return MPIGX_ERR_WIN;
   if (flavor) *flavor = w->flavor;
   return MPIGX_SUCCESS;
 }
 
 int mpigx_win_free(mpigx_win_t* pw) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (!pw) return MPIGX_ERR_ARG;
   mpigx_win* w = *pw;
   int rc = check_win(w);
@@ -734,7 +735,7 @@ int mpigx_win_free(mpigx_win_t* pw) {
 }
 
 int mpigx_win_attach(mpigx_win_t w, void* base, long long size) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   if (w->flavor != MPIGX_WIN_FLAVOR_DYNAMIC) return MPIGX_ERR_RMA_FLAVOR;
@@ -772,7 +773,7 @@ int mpigx_win_attach(mpigx_win_t w, void* base, long long size) {
 }
 
 int mpigx_win_detach(mpigx_win_t w, const void* base) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   if (w->flavor != MPIGX_WIN_FLAVOR_DYNAMIC) return MPIGX_ERR_RMA_FLAVOR;
@@ -790,7 +791,7 @@ int mpigx_win_detach(mpigx_win_t w, const void* base) {
 }
 
 int mpigx_win_fence(int assert_, mpigx_win_t w) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   (void)assert_;
   int rc = check_win(w);
   if (rc) return rc;
@@ -807,7 +808,7 @@ int mpigx_win_fence(int assert_, mpigx_win_t w) {
 }
 
 int mpigx_win_lock(int lock_type, int rank, int assert_, mpigx_win_t w) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   // MPICH 3.3.2 reports a bad lock type as MPI_ERR_OTHER ("**locktype")
@@ -827,7 +828,7 @@ int mpigx_win_lock(int lock_type, int rank, int assert_, mpigx_win_t w) {
 }
 
 int mpigx_win_unlock(int rank, mpigx_win_t w) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   rc = check_target(w, rank);
@@ -851,7 +852,7 @@ int mpigx_win_unlock(int rank, mpigx_win_t w) {
 }
 
 int mpigx_win_flush(int rank, mpigx_win_t w) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   rc = check_target(w, rank);
@@ -865,7 +866,7 @@ int mpigx_win_flush(int rank, mpigx_win_t w) {
 }
 
 int mpigx_win_sync(mpigx_win_t w) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   rt::progress_all(w->c);
@@ -876,7 +877,7 @@ int mpigx_win_sync(mpigx_win_t w) {
 
 int mpigx_get(void* origin_addr, int origin_count, int origin_datatype, int target_rank, long long target_disp,
               int target_count, int target_datatype, mpigx_win_t w) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   int es;
@@ -895,7 +896,7 @@ int mpigx_get(void* origin_addr, int origin_count, int origin_datatype, int targ
 
 int mpigx_put(const void* origin_addr, int origin_count, int origin_datatype, int target_rank,
               long long target_disp, int target_count, int target_datatype, mpigx_win_t w) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   int rc = check_win(w);
   if (rc) return rc;
   int es;
@@ -959,7 +960,7 @@ static int acc_common(const void* origin, int ocount, int otype, void* result, i
 
 int mpigx_accumulate(const void* origin_addr, int origin_count, int origin_datatype, int target_rank,
                      long long target_disp, int target_count, int target_datatype, int op, mpigx_win_t win) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   if (op == MPIGX_NO_OP) return MPIGX_ERR_OP;  // MPI_NO_OP only fetches: MPICH rejects it here
   return acc_common(origin_addr, origin_count, origin_datatype, nullptr, target_count, target_datatype, target_rank,
                     target_disp, target_count, target_datatype, op, win, false);
@@ -968,14 +969,14 @@ int mpigx_accumulate(const void* origin_addr, int origin_count, int origin_datat
 int mpigx_get_accumulate(const void* origin_addr, int origin_count, int origin_datatype, void* result_addr,
                          int result_count, int result_datatype, int target_rank, long long target_disp,
                          int target_count, int target_datatype, int op, mpigx_win_t win) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   return acc_common(origin_addr, origin_count, origin_datatype, result_addr, result_count, result_datatype,
                     target_rank, target_disp, target_count, target_datatype, op, win, true);
 }
 
 int mpigx_fetch_and_op(const void* origin_addr, void* result_addr, int datatype, int target_rank,
                        long long target_disp, int op, mpigx_win_t win) {
-  std::lock_guard<std::recursive_mutex> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
+  std::lock_guard<rt::BigLock> big(rt::big_lock());  // THREAD_MULTIPLE (runtime.hpp)
   return acc_common(origin_addr, 1, datatype, result_addr, 1, datatype, target_rank, target_disp, 1, datatype, op,
                     win, true);
 }

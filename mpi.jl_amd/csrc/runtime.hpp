@@ -313,7 +313,34 @@ void progress_all(mpigx_comm* c);
 // thread blocked in Wait never holds up another thread's Isend.  Collectives
 // take it only for their progress passes (one call at a time per
 // communicator, as MPI requires).
-std::recursive_mutex& big_lock();
+// Recursive, and YIELDABLE: a thread that waits inside a locked call (an RMA
+// fence or lock, a host exchange) gives the lock up while it polls
+// (yield_big_lock), so that e.g. one thread in Win_fence never blocks another
+// thread's Isend that a peer needs before it can reach the fence.
+struct BigLock {
+  std::mutex m;
+  std::atomic<std::thread::id> owner{};
+  int depth = 0;
+  void lock() {
+    if (owner.load(std::memory_order_relaxed) == std::this_thread::get_id()) {
+      ++depth;
+      return;
+    }
+    m.lock();
+    owner.store(std::this_thread::get_id(), std::memory_order_relaxed);
+    depth = 1;
+  }
+  void unlock() {
+    if (--depth == 0) {
+      owner.store(std::thread::id(), std::memory_order_relaxed);
+      m.unlock();
+    }
+  }
+};
+BigLock& big_lock();
+// In a wait loop: if this thread holds the big lock, release it completely,
+// let other threads in, and take it back at the same depth.
+void yield_big_lock();
 // Some peer of c can no longer take part: its process is gone or its
 // communicator failed (shm flags).  Point-to-point and RMA waits use it as
 // their only way out: like the collectives they wait for a live late peer.

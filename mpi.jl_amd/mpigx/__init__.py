@@ -11,8 +11,13 @@ from .api import *  # noqa: F401,F403
 from .p2p import *  # noqa: F401,F403
 from .rma import *  # noqa: F401,F403
 from .types import Types  # noqa: F401
-from .api import (COMM_WORLD, IN_PLACE, Barrier, Buffer, Comm, Datatype, MPIError, Op, error_string,
+from .api import (IN_PLACE, Barrier, Buffer, Comm, Datatype, MPIError, Op, error_string,
                   reduce_local_multi)
+
+# COMM_WORLD must not be a module attribute here: Init() rebinds
+# api.COMM_WORLD, and __getattr__ below (consulted only for names the module
+# does not have) hands out the live value, as MPI.COMM_WORLD is in MPI.jl
+globals().pop("COMM_WORLD", None)
 
 
 def free(obj):

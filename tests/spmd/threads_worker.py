@@ -6,7 +6,9 @@ them on the main thread.  ctypes releases the GIL around each call, so the
 threads really are inside libmpigx together (rt::big_lock, runtime.hpp).
 Beyond the reference's N = 10: the same with 256 pairs, 8 threads and three
 rounds, and a thread that waits on its own receive while other threads keep
-posting.  Launched by tests/test_reference_suite_gpu.py."""
+posting, and a thread in Win_fence while another sends the message the
+peer needs before its own fence.  Launched by
+tests/test_reference_suite_gpu.py."""
 import json
 import os
 import sys
@@ -70,6 +72,27 @@ def main():
         MPI.Wait_(MPI.Isend(out, dst, 9000, comm))
         waiter.join(60)
         check(not waiter.is_alive() and bool((got == float(src)).all()), "blocked waiter + concurrent Isend")
+        # one thread in a collective RMA call that waits (Win_fence), another
+        # sending the message its peer needs before the peer can reach the
+        # fence: the waiting call must let the Isend through (the big lock
+        # is yielded while it polls, rt::yield_big_lock)
+        win_buf = torch.zeros(64, dtype=torch.float64, device="cuda")
+        win = MPI.Win_create(win_buf, comm)
+        MPI.Win_fence(0, win)
+        token = torch.full((8,), 5.0 + rank, dtype=torch.float64, device="cuda")
+        if rank == 0:
+            fencer = threading.Thread(target=lambda: MPI.Win_fence(0, win))
+            fencer.start()
+            for q in range(1, size):
+                MPI.Send(token, q, 9100, comm)
+            fencer.join(60)
+            check(not fencer.is_alive(), "fence with a concurrent Send on another thread")
+        else:
+            got2 = torch.zeros(8, dtype=torch.float64, device="cuda")
+            MPI.Recv_(got2, 0, 9100, comm)
+            check(bool((got2 == 5.0).all()), "message sent beside a fence")
+            MPI.Win_fence(0, win)
+        MPI.free(win)
     MPI.Barrier(comm)
     MPI.Finalize()
     print(json.dumps({"rank": MPI.Comm_rank(comm), "provided": provided, "checks": NCHECK[0],

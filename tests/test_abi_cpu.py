@@ -230,3 +230,18 @@ def test_count_is_a_cint():
     for bad in (1 << 31, -(1 << 31) - 1, 1 << 40):
         with pytest.raises(api.InexactError):
             api._cint(bad)
+
+
+def test_comm_world_is_live():
+    """MPI.COMM_WORLD is the communicator Init() / Init_thread() built (MPI.jl's
+    MPI.COMM_WORLD), not a copy of the pre-Init placeholder."""
+    from mpigx import api
+    saved = api.COMM_WORLD
+    try:
+        api.COMM_WORLD = "built-by-Init"
+        assert mpigx.COMM_WORLD == "built-by-Init"
+    finally:
+        api.COMM_WORLD = saved
+    assert mpigx.THREAD_SINGLE < mpigx.THREAD_FUNNELED < mpigx.THREAD_SERIALIZED < mpigx.THREAD_MULTIPLE == 3
+    v = ctypes.c_int(-1)
+    assert mpigx.lib().mpigx_query_thread(ctypes.byref(v)) == 0 and v.value == 3
