@@ -81,7 +81,11 @@ __global__ __launch_bounds__(256) void exp4(P8 a) {
     f32x4* q = a.out + j;
     if constexpr (SP == 0) *q = r;
     else if constexpr (SP == 1) __builtin_nontemporal_store(r, q);
-    else asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(q), "v"(r) : "memory");
+    else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(q), "v"(r) : "memory");
+    else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(q), "v"(r) : "memory");
+    else if constexpr (SP == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" : : "v"(q), "v"(r) : "memory");
+    else if constexpr (SP == 5) asm volatile("global_store_dwordx4 %0, %1, off sc0" : : "v"(q), "v"(r) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" : : "v"(q), "v"(r) : "memory");
   }
 }
 
@@ -188,6 +192,10 @@ int main(int argc, char** argv) {
       {"exp plain shift0", B9, [&] { hipLaunchKernelGGL((exp4<0, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp nt shift0", B9, [&] { hipLaunchKernelGGL((exp4<1, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp sc1 shift0", B9, [&] { hipLaunchKernelGGL((exp4<2, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp sc0sc1", B9, [&] { hipLaunchKernelGGL((exp4<3, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp sc1nt", B9, [&] { hipLaunchKernelGGL((exp4<4, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp sc0", B9, [&] { hipLaunchKernelGGL((exp4<5, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"exp sc0sc1nt", B9, [&] { hipLaunchKernelGGL((exp4<6, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp plain shift16M", B9, [&] { hipLaunchKernelGGL((exp4<0, (1 << 20)>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp plain shift68K", B9, [&] { hipLaunchKernelGGL((exp4<0, 4352>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp sc1 shift16M", B9, [&] { hipLaunchKernelGGL((exp4<2, (1 << 20)>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
