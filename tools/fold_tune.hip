@@ -89,6 +89,35 @@ __global__ __launch_bounds__(256) void exp4(P8 a) {
   }
 }
 
+// write bursts: each thread folds T consecutive tiles (U = 4 vectors each)
+// and keeps the results in registers, then stores all 4T of them together —
+// the write stream reaches HBM in bursts of T tiles per wave instead of one
+// store group after every 32 loads (fewer read/write turnarounds, if that is
+// what costs the fold its gap to the read-only stream)
+template <int T>
+__global__ __launch_bounds__(256) void expb(P8 a) {
+  f32x4 res[T][4];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const long long base = ((long long)blockIdx.x * T + t) * 1024 + threadIdx.x;
+    f32x4 v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[u][k] = __builtin_nontemporal_load(a.in[k] + base + u * 256);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      res[t][u] = ((v[u][0] + v[u][1]) + (v[u][2] + v[u][3])) + ((v[u][4] + v[u][5]) + (v[u][6] + v[u][7]));
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      f32x4* q = a.out + ((long long)blockIdx.x * T + t) * 1024 + threadIdx.x + u * 256;
+      asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(q), "v"(res[t][u]) : "memory");
+    }
+}
+
 // exhaustive f32 -> bf16: hardware pair conversion vs the software RNE; each
 // thread checks 16 pairs, one atomic per block (bounded even if all differ)
 __global__ __launch_bounds__(256) void cvt_check(unsigned long long base, unsigned long long* bad, unsigned* first) {
@@ -196,6 +225,9 @@ int main(int argc, char** argv) {
       {"exp sc1nt", B9, [&] { hipLaunchKernelGGL((exp4<4, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp sc0", B9, [&] { hipLaunchKernelGGL((exp4<5, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp sc0sc1nt", B9, [&] { hipLaunchKernelGGL((exp4<6, 0>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"burst T2", B9, [&] { hipLaunchKernelGGL((expb<2>), dim3(G4 / 2), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"burst T4", B9, [&] { hipLaunchKernelGGL((expb<4>), dim3(G4 / 4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
+      {"burst T8", B9, [&] { hipLaunchKernelGGL((expb<8>), dim3(G4 / 8), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp plain shift16M", B9, [&] { hipLaunchKernelGGL((exp4<0, (1 << 20)>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp plain shift68K", B9, [&] { hipLaunchKernelGGL((exp4<0, 4352>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
       {"exp sc1 shift16M", B9, [&] { hipLaunchKernelGGL((exp4<2, (1 << 20)>), dim3(G4), dim3(256), 0, 0, pa); return hipGetLastError(); }},
