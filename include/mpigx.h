@@ -194,7 +194,12 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
                                         on another GPU (uncached signal arrays and LL areas, the
                                         one-rank-per-GPU protocol) even when it shares this one; a test
                                         knob that runs the production signalling on a 1-GPU box (init only) */
-#define MPIGX_KNOB_COUNT 20
+#define MPIGX_KNOB_CONCURRENT_COMMS 20 /* MPIGX_CONCURRENT_COMMS: >= 1 (default 1), how many communicators'
+                                        * collectives may run on a GPU at the same time (threads, or
+                                        * stream-ordered launches on different streams); every spinning
+                                        * kernel's grid is capped at 1/this of the device's resident blocks,
+                                        * so all of them fit at once (init-only) */
+#define MPIGX_KNOB_COUNT 21
 #define MPIGX_ALGO_AUTO 0     /* unset: static rules + the measured choices */
 #define MPIGX_ALGO_LL 1       /* "ll" */
 #define MPIGX_ALGO_LL2 2      /* "ll2" */

@@ -549,8 +549,15 @@ int finish(mpigx_comm* c) {
 // gave up 30 s later; nothing about 2 ranks makes that impossible — any other
 // resident kernel (a peer's torch work) takes the slot a spinning grid needs.
 // MPIGX_SHARE_HEADROOM = 0 turns it off (measurement only).
+// Concurrent communicators (MPIGX_CONCURRENT_COMMS = K, agreed): collectives
+// of K communicators may spin on one GPU at once (threads, or stream-ordered
+// launches on separate streams); a kernel's blocks wait only for the same
+// blocks of ITS peers, so all K kernels must fit together or a GPU can fill up
+// with blocks whose partners are not resident anywhere (seen with 3 ranks x 3
+// communicators on one GPU: every rank's GPU in a launch, none moving).  The
+// share of every communicator is therefore one K-th of the device.
 int kernel_cap(mpigx_comm* c, int occ) {
-  const long long share = c->dev_share > 0 ? c->dev_share : 1;
+  const long long share = (long long)(c->dev_share > 0 ? c->dev_share : 1) * (c->concurrent_comms > 0 ? c->concurrent_comms : 1);
   long long cap;
   const bool headroom = c->share_headroom != 0;
   if (share > 1 && headroom)
@@ -1986,7 +1993,8 @@ const char* const kKnobEnv[MPIGX_KNOB_COUNT] = {
     "MPIGX_ALGO",   "MPIGX_BCAST",      "MPIGX_RING_CHANNELS", "MPIGX_MAX_BLOCKS",     "MPIGX_ONESHOT_MAX",
     "MPIGX_ZC_MIN", "MPIGX_BCAST_SAG_MIN", "MPIGX_ZC_REQUIRE", "MPIGX_BYTES_PER_BLOCK", "MPIGX_LL_AUTO",
     "MPIGX_AR_TUNE", "MPIGX_ZC_OPTIMISTIC", "MPIGX_SYNC_SPIN", "MPIGX_STAGING_BYTES",  "MPIGX_LL_MAX",
-    "MPIGX_AR_SLICES", "MPIGX_SCAN_PP", "MPIGX_SHARE_HEADROOM", "MPIGX_SHARED_GATE", "MPIGX_PEER_MEM"};
+    "MPIGX_AR_SLICES", "MPIGX_SCAN_PP", "MPIGX_SHARE_HEADROOM", "MPIGX_SHARED_GATE", "MPIGX_PEER_MEM",
+    "MPIGX_CONCURRENT_COMMS"};
 
 long long knob_value(const mpigx_comm* c, int k) {
   switch (k) {
@@ -2010,6 +2018,7 @@ long long knob_value(const mpigx_comm* c, int k) {
     case MPIGX_KNOB_SHARE_HEADROOM: return c->share_headroom;
     case MPIGX_KNOB_SHARED_GATE: return c->shared_gate ? 1 : 0;
     case MPIGX_KNOB_PEER_MEM: return c->peer_mem;
+    case MPIGX_KNOB_CONCURRENT_COMMS: return c->concurrent_comms;
     default: return -1;
   }
 }
@@ -2104,6 +2113,10 @@ int knob_apply(mpigx_comm* c, int k, long long v, bool init) {
       if (!init || !in(0, 1)) return MPIGX_ERR_ARG;
       c->peer_mem = (int)v;
       return MPIGX_SUCCESS;
+    case MPIGX_KNOB_CONCURRENT_COMMS:  // init-only: the grids of every launch depend on it
+      if (!init || !in(1, 64)) return MPIGX_ERR_ARG;
+      c->concurrent_comms = (int)v;
+      return MPIGX_SUCCESS;
     default: return MPIGX_ERR_ARG;
   }
 }
@@ -2178,6 +2191,10 @@ int knobs_from_env(mpigx_comm* c) {
     c->share_headroom = h < 0 ? -1 : h > 0 ? 1 : 0;
   }
   c->shared_gate = env_ll("MPIGX_SHARED_GATE", 1) != 0;
+  {
+    const long long cc = env_ll("MPIGX_CONCURRENT_COMMS", 1);
+    c->concurrent_comms = (int)(cc < 1 ? 1 : cc > 64 ? 64 : cc);
+  }
   // "xdev": every peer takes the cross-device protocol (uncached signal
   // arrays and LL areas, comm_init) — what one rank per GPU runs, exercised
   // on the 1-GPU test box

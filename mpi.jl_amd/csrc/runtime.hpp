@@ -273,6 +273,7 @@ struct mpigx_comm {
   int share_headroom = -1;              // MPIGX_SHARE_HEADROOM: ranks sharing a device leave one block per CU free (-1 auto: >= 4 ranks)
   bool scan_pp = true;                  // MPIGX_SCAN_PP: pull-push Scan / Exscan (kernels.hpp scan_pp_body)
   bool shared_gate = true;              // MPIGX_SHARED_GATE: ranks sharing a device meet on the host first
+  int concurrent_comms = 1;             // MPIGX_CONCURRENT_COMMS: grid caps divided by it (kernel_cap)
   int peer_mem = 0;                     // MPIGX_PEER_MEM: 0 auto (memory type per pair), 1 xdev (every peer as
                                         // if on another GPU: uncached signal / LL arrays; test knob)
   bool diag_trace = false;              // MPIGX_DIAG_TRACE: one stderr line per launch (diagnostic)

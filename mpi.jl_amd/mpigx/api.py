@@ -593,7 +593,7 @@ def set_reduce_order(comm: Comm, order: int):
 KNOBS = {"ALGO": 0, "BCAST": 1, "RING_CHANNELS": 2, "MAX_BLOCKS": 3, "ONESHOT_MAX": 4, "ZC_MIN": 5,
          "BCAST_SAG_MIN": 6, "ZC_REQUIRE": 7, "BYTES_PER_BLOCK": 8, "LL_AUTO": 9, "AR_TUNE": 10,
          "ZC_OPTIMISTIC": 11, "SYNC_SPIN": 12, "STAGING_BYTES": 13, "LL_MAX": 14, "AR_SLICES": 15,
-         "SCAN_PP": 16, "SHARE_HEADROOM": 17, "SHARED_GATE": 18, "PEER_MEM": 19}
+         "SCAN_PP": 16, "SHARE_HEADROOM": 17, "SHARED_GATE": 18, "PEER_MEM": 19, "CONCURRENT_COMMS": 20}
 ALGOS = {None: 0, "": 0, "auto": 0, "ll": 1, "ll2": 2, "oneshot": 3, "twoshot": 4, "push": 5, "ring": 6,
          "pull": 7, "pull_generic": 8, "pullpush": 9}
 BCAST_MODES = {None: 0, "": 0, "auto": 0, "direct": 1, "sag": 2, "relay": 3}

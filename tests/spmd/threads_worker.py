@@ -7,7 +7,9 @@ threads really are inside libmpigx together (rt::big_lock, runtime.hpp).
 Beyond the reference's N = 10: the same with 256 pairs, 8 threads and three
 rounds, and a thread that waits on its own receive while other threads keep
 posting, and a thread in Win_fence while another sends the message the
-peer needs before its own fence.  Launched by
+peer needs before its own fence, and collectives on three duplicated
+communicators from three threads at once (MPIGX_CONCURRENT_COMMS=4 set by
+the launcher so the three grids fit on the GPU together).  Launched by
 tests/test_reference_suite_gpu.py."""
 import json
 import os
@@ -93,6 +95,40 @@ def main():
             check(bool((got2 == 5.0).all()), "message sent beside a fence")
             MPI.Win_fence(0, win)
         MPI.free(win)
+        # collectives on distinct communicators from distinct threads at once
+        # (each communicator's calls stay ordered, as MPI requires): every
+        # thread runs a loop of Allreduce! (LL, one-shot and zero-copy sizes)
+        # and Bcast! on its own Comm_dup of COMM_WORLD
+        comms = [MPI.Comm_dup(comm) for _ in range(3)]
+        results = [None] * len(comms)
+
+        def loop(i):
+            cm = comms[i]
+            ok = True
+            # each thread on its own stream (the mirror runs a communicator's
+            # collectives on the caller's current stream; two communicators'
+            # kernels queued on ONE stream in different orders on different
+            # ranks would wait for each other — the rule NCCL / RCCL state
+            # for concurrent communicators too)
+            torch.cuda.set_stream(torch.cuda.Stream())
+            for it, cnt in enumerate((7, 1000, 60000, (32 << 20) // 4, 5)):
+                x = torch.full((cnt,), float(rank + 1 + i), device="cuda")
+                y = MPI.Allreduce(x, MPI.SUM, cm)
+                ok &= bool((y == float(sum(q + 1 + i for q in range(size)))).all())
+                b = torch.full((cnt,), float(it) if rank == 0 else -1.0, device="cuda")
+                MPI.Bcast_(b, 0, cm)
+                ok &= bool((b == float(it)).all())
+            torch.cuda.synchronize()
+            results[i] = ok
+
+        ths = [threading.Thread(target=loop, args=(i,)) for i in range(len(comms))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(120)
+        check(all(results) and not any(t.is_alive() for t in ths), f"concurrent collectives on {len(comms)} comms: {results}")
+        for cm in comms:
+            MPI.free(cm)
     MPI.Barrier(comm)
     MPI.Finalize()
     print(json.dumps({"rank": MPI.Comm_rank(comm), "provided": provided, "checks": NCHECK[0],

@@ -30,7 +30,9 @@ def test_reference_threads_device(n):
     """test/test_threads.jl in device mode (tests/spmd/threads_worker.py):
     Init_thread(THREAD_MULTIPLE), threaded Irecv! / Isend of one-element
     device views, Waitall on the main thread."""
-    env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "30000"}
+    # the worker runs collectives of three communicators at once: their
+    # spinning kernels must fit on the GPU together (MPIGX_CONCURRENT_COMMS)
+    env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "30000", "MPIGX_CONCURRENT_COMMS": "4"}
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "threads_worker.py"), n, timeout=300, extra_env=env)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
     assert all(rc == 0 for rc in rcs), "\n".join(o[-2000:] for o in outs)
