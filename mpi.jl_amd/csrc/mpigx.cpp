@@ -27,6 +27,8 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -307,37 +309,94 @@ int shared_gate(mpigx_comm* c) {
 
 // Stream-ordered (RCCL-style) launches wait for a late peer too (round 5):
 // like ncclAllReduce they have no time limit — nobody waits on the host for
-// them — and this thread, started with the communicator's first
-// stream-ordered launch, does what finish() does for a blocking call: it
-// publishes the launch this rank's GPU has reached (ShmRank.kseq_run) and
-// stores the cancel word when the wait cannot end, i.e. when a peer's
-// communicator failed or its process is gone (checked every 0.25 s).  The
-// cancelled kernels record a timeout in the error word, which the next
-// synchronizing call reports (mpigx_comm_synchronize / any blocking call),
-// breaking the communicator.  Unlike a blocking call there is no stall
-// detection: a stream-ordered launch that never completes for a protocol
-// reason hangs, as an RCCL kernel would.
-void watch_peers(mpigx_comm* c) {
-  unsigned tick = 0;
-  while (!c->watcher_stop.load(std::memory_order_acquire)) {
-    usleep(10000);
-    if (!c->shm) continue;
-    c->shm->ranks[c->rank].kseq_run.store(*c->started, std::memory_order_release);
-    if (__atomic_load_n(c->cancel, __ATOMIC_ACQUIRE)) continue;  // already cancelled (finish or here)
-    if (++tick % 25) continue;
-    int who = peer_broken(c);
-    const char* why = who >= 0 ? "its communicator failed" : nullptr;
-    for (int q = 0; !why && q < c->n; ++q)
-      if (q != c->rank && peer_gone(c, q)) {
-        who = q;
-        why = "its process is gone";
-      }
-    if (why) {
-      fprintf(stderr, "[mpigx] rank %d: cancelling stream-ordered waits: rank %d: %s\n", c->rank, who, why);
-      __atomic_store_n(c->cancel, 1u, __ATOMIC_RELEASE);
+// them — and one process-wide watcher thread does for every communicator
+// that has made a stream-ordered launch what finish() does for a blocking
+// call: it publishes the launch this rank's GPU has reached
+// (ShmRank.kseq_run) and stores the cancel word when the wait cannot end,
+// i.e. when a peer's communicator failed or its process is gone (checked
+// every 0.25 s).  The cancelled kernels record a timeout in the error word,
+// which the next synchronizing call reports (mpigx_comm_synchronize / any
+// blocking call), breaking the communicator.  Unlike a blocking call there
+// is no stall detection: a stream-ordered launch that never completes for a
+// protocol reason hangs, as an RCCL kernel would.
+// One thread for the process however many communicators there are (an
+// application with hundreds of Comm_split results must not get hundreds of
+// 100 Hz threads); it runs while at least one communicator is registered
+// and exits by itself when the last is released.  The registry is never
+// destroyed (a static destructor at exit would race the detached thread).
+namespace {
+struct PeerWatch {
+  std::mutex m;
+  std::vector<mpigx_comm*> comms;
+  bool running = false;
+};
+PeerWatch& peer_watch() {
+  static PeerWatch* w = new PeerWatch;
+  return *w;
+}
+void watch_one(mpigx_comm* c, bool check) {
+  if (!c->shm) return;
+  c->shm->ranks[c->rank].kseq_run.store(*c->started, std::memory_order_release);
+  if (!check || __atomic_load_n(c->cancel, __ATOMIC_ACQUIRE)) return;  // already cancelled (finish or here)
+  int who = peer_broken(c);
+  const char* why = who >= 0 ? "its communicator failed" : nullptr;
+  for (int q = 0; !why && q < c->n; ++q)
+    if (q != c->rank && peer_gone(c, q)) {
+      who = q;
+      why = "its process is gone";
     }
+  if (why) {
+    fprintf(stderr, "[mpigx] rank %d: cancelling stream-ordered waits: rank %d: %s\n", c->rank, who, why);
+    __atomic_store_n(c->cancel, 1u, __ATOMIC_RELEASE);
   }
 }
+void watch_peers() {
+  PeerWatch& w = peer_watch();
+  for (unsigned tick = 1;; ++tick) {
+    usleep(10000);
+    std::lock_guard<std::mutex> g(w.m);
+    if (w.comms.empty()) {
+      w.running = false;
+      return;
+    }
+    for (mpigx_comm* c : w.comms) watch_one(c, tick % 25 == 0);
+  }
+}
+// make_view of a stream-ordered launch: register c (once)
+void watch_register(mpigx_comm* c) {
+  PeerWatch& w = peer_watch();
+  std::lock_guard<std::mutex> g(w.m);
+  if (c->watched) return;
+  c->watched = true;
+  w.comms.push_back(c);
+  if (!w.running) {
+    w.running = true;
+    std::thread(watch_peers).detach();
+  }
+  static const bool at_exit = [] {
+    // a process that exits without freeing its communicators: stop watching
+    // before the runtime frees the pinned words the watcher reads (exit
+    // handlers run in reverse order, and the HIP runtime registered its own
+    // before this one)
+    std::atexit([] {
+      PeerWatch& pw = peer_watch();
+      std::lock_guard<std::mutex> l(pw.m);
+      for (mpigx_comm* x : pw.comms) x->watched = false;
+      pw.comms.clear();
+    });
+    return true;
+  }();
+  (void)at_exit;
+}
+// comm_release: once this returns the watcher never touches c again
+void watch_unregister(mpigx_comm* c) {
+  if (!c->watched) return;
+  PeerWatch& w = peer_watch();
+  std::lock_guard<std::mutex> g(w.m);
+  w.comms.erase(std::remove(w.comms.begin(), w.comms.end(), c), w.comms.end());
+  c->watched = false;
+}
+}  // namespace
 
 PeerView make_view(mpigx_comm* c) {
   if (c->diag_trace) {  // before every launch: the peers' canaries through my mappings of their signal arrays
@@ -379,7 +438,7 @@ PeerView make_view(mpigx_comm* c) {
   // call's host watches the peers while it waits (finish), a stream-ordered
   // launch's peers are watched by watch_peers (started here, once)
   pv.cancel = c->cancel_dev;
-  if (!pv.done && c->n > 1 && c->shm && !c->watcher) c->watcher = new std::thread(watch_peers, c);
+  if (!pv.done && c->n > 1 && c->shm && !c->watched) watch_register(c);
   pv.stamps = c->stamps;
   // each peer gets its words in the array of ITS memory type for me: ordinary
   // memory between ranks of one device, uncached across devices (one memory
@@ -2216,12 +2275,7 @@ int knobs_from_env(mpigx_comm* c) {
 void comm_release(mpigx_comm* c) {
   (void)hipSetDevice(c->device);
   if (c->stream || c->launch_seq) (void)hipStreamSynchronize(c->stream);
-  if (c->watcher) {  // after the drain: a waiting stream-ordered launch needs it to be cancelled
-    c->watcher_stop.store(true, std::memory_order_release);
-    c->watcher->join();
-    delete c->watcher;
-    c->watcher = nullptr;
-  }
+  watch_unregister(c);  // after the drain: a waiting stream-ordered launch needs the watcher to be cancelled
   rt::rma_destroy(c);
   rt::p2p_destroy(c);
   for (int q = 0; q < c->n; ++q) {

@@ -286,10 +286,9 @@ struct mpigx_comm {
   // tools/ipc_torch.py); MPIGX_IPC_ALLOC_MAX overrides (tests).
   long long ipc_alloc_max = 0;
   int hip_runtime = 0;                  // hipRuntimeGetVersion of the runtime this process loaded
-  // Stream-ordered launches' peer watcher (mpigx.cpp watch_peers): started
-  // with the first stream-ordered launch, stopped in comm_release.
-  std::thread* watcher = nullptr;
-  std::atomic<bool> watcher_stop{false};
+  // Registered with the process-wide peer watcher (mpigx.cpp watch_peers)
+  // at the first stream-ordered launch, unregistered in comm_release.
+  bool watched = false;
   std::mutex mu;
 };
 
