@@ -193,10 +193,13 @@ void put_event(P2PState* P, hipEvent_t& e) {
   e = nullptr;
 }
 
-char* pack_get(P2PState* P, long long bytes, long long* cap) {
+// max_cap > 0: only a temporary no larger than that (one the runtime can
+// IPC-map, runtime.hpp ipc_alloc_max)
+char* pack_get(P2PState* P, long long bytes, long long* cap, long long max_cap = 0) {
   size_t best = P->packpool.size();
   for (size_t i = 0; i < P->packpool.size(); ++i)
-    if (P->packpool[i].first >= bytes && (best == P->packpool.size() || P->packpool[i].first < P->packpool[best].first))
+    if (P->packpool[i].first >= bytes && (max_cap <= 0 || P->packpool[i].first <= max_cap) &&
+        (best == P->packpool.size() || P->packpool[i].first < P->packpool[best].first))
       best = i;
   if (best < P->packpool.size()) {
     char* p = P->packpool[best].second;
@@ -599,7 +602,7 @@ int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpi
   }
   if (r->bytes > 0) {
     if (!td.contig) {  // derived, non-contiguous: pack on device into a pooled temporary
-      r->pack_tmp = pack_get(P, r->bytes, &r->pack_cap);
+      r->pack_tmp = pack_get(P, r->bytes, &r->pack_cap, c->ipc_alloc_max);
       if (!r->pack_tmp) {
         delete r;
         return MPIGX_ERR_NO_MEM;
@@ -624,7 +627,7 @@ int mpigx_isend(const void* buf, int count, int datatype, int dest, int tag, mpi
       bool ok = false;
       const long long rounded = (r->bytes + (1 << 20) - 1) & ~((1ll << 20) - 1);  // pack_get's allocation
       if (!r->pack_tmp && (c->ipc_alloc_max <= 0 || rounded <= c->ipc_alloc_max)) {
-        r->pack_tmp = pack_get(P, r->bytes, &r->pack_cap);
+        r->pack_tmp = pack_get(P, r->bytes, &r->pack_cap, c->ipc_alloc_max);
         if (r->pack_tmp && hipMemcpyAsync(r->pack_tmp, buf, r->bytes, hipMemcpyDeviceToDevice, c->stream) == hipSuccess &&
             hipStreamSynchronize(c->stream) == hipSuccess) {
           r->sbuf = r->pack_tmp;
