@@ -435,7 +435,10 @@ def bench_allreduce(args):
 
     def xgmi_section():
         c0 = XC.read(bus)
-        if c0 is None:
+        # every rank takes the same branch: a rank whose metrics read failed
+        # must not skip the collectives below while its peers wait in them
+        (missing,) = tmax(1.0 if c0 is None else 0.0)
+        if missing:
             return None
         reps = max(args.steps, 10)
         xs = rank_input(rank, S // 4)
