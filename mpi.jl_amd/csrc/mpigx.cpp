@@ -1688,6 +1688,18 @@ int reduce_common(mpigx_comm* c, const void* send, void* recv, long long count, 
 int check_comm(mpigx_comm* c) {
   if (!c) return MPIGX_ERR_COMM;
   if (c->broken) return MPIGX_ERR_OTHER;
+  // A call cannot be captured into a HIP graph: every launch carries a fresh
+  // epoch and argument block, which a replay would repeat (the peers would
+  // wait for epochs that never come), and blocking calls wait on the host.
+  // Refused before anything is enqueued, so the capture and the
+  // communicator both stay usable.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(c->stream, &cap) != hipSuccess) (void)hipGetLastError();
+  else if (cap != hipStreamCaptureStatusNone) {
+    fprintf(stderr, "[mpigx] rank %d: the stream is being captured into a HIP graph; mpigx calls cannot be "
+            "captured (issue them outside the capture)\n", c->rank);
+    return MPIGX_ERR_OTHER;
+  }
   c->t_entry = now_s();  // host-cost diagnostic (mpigx_comm_host_stats)
   c->launch_pending = true;
   if (hipSetDevice(c->device) != hipSuccess) return MPIGX_ERR_INTERN;
