@@ -7,6 +7,7 @@
   op x type matrix recorded in tests/golden/op_type_matrix.json.
 """
 import ctypes
+import os
 import re
 
 import pytest
@@ -245,3 +246,18 @@ def test_comm_world_is_live():
     assert mpigx.THREAD_SINGLE < mpigx.THREAD_FUNNELED < mpigx.THREAD_SERIALIZED < mpigx.THREAD_MULTIPLE == 3
     v = ctypes.c_int(-1)
     assert mpigx.lib().mpigx_query_thread(ctypes.byref(v)) == 0 and v.value == 3
+
+
+def test_knob_env_names_follow_the_header_and_are_documented():
+    """mpigx.cpp kKnobEnv[k] is the environment variable of MPIGX_KNOB_* index k
+    (init reads it, and names it when ranks disagree), and INTEGRATION.md's
+    knob table documents every one of them."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "mpi.jl_amd", "csrc", "mpigx.cpp")).read()
+    m = re.search(r"kKnobEnv\[MPIGX_KNOB_COUNT\]\s*=\s*\{(.*?)\};", src, flags=re.S)
+    assert m, "kKnobEnv table not found"
+    env = re.findall(r'"(MPIGX_\w+)"', m.group(1))
+    by_index = {v: k for k, v in mpigx.KNOBS.items()}
+    assert env == ["MPIGX_" + by_index[i] for i in range(len(by_index))]
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    assert [e for e in env if f"| `{e}` |" not in doc] == []
