@@ -19,14 +19,17 @@ from spmd_launch import ROOT, launch
 pytestmark = pytest.mark.gpu
 
 ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS": "30000",
-       "MPIGX_ZC_MIN": str(1 << 20), "FUZZ_CASES": "120"}
+       "MPIGX_ZC_MIN": str(1 << 20), "FUZZ_CASES": os.environ.get("FUZZ_CASES", "120")}
+# a longer campaign: FUZZ_SEED_BASE shifts every seed, FUZZ_CASES raises the
+# case count (profiles/r05zo_*)
+SEED_BASE = int(os.environ.get("FUZZ_SEED_BASE", 0))
 XDEV = dict(ENV, MPIGX_PEER_MEM="xdev", MPIGX_SHARED_GATE="0")
 
 
 @pytest.mark.parametrize("cfg,n,seed", [("same", 2, 11), ("same", 3, 12), ("same", 5, 13), ("same", 8, 14),
                                         ("xdev", 3, 15), ("xdev", 8, 16)])
 def test_fuzz_collectives(cfg, n, seed):
-    env = dict(ENV if cfg == "same" else XDEV, FUZZ_SEED=str(seed))
+    env = dict(ENV if cfg == "same" else XDEV, FUZZ_SEED=str(seed + SEED_BASE))
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "fuzz_worker.py"), n, timeout=600, extra_env=env)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     assert all(rc == 0 for rc in rcs), msg
