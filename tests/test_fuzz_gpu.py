@@ -35,4 +35,6 @@ def test_fuzz_collectives(cfg, n, seed):
     assert all(rc == 0 for rc in rcs), msg
     res = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"nfail"' in l]
     assert len(res) == n, msg
+    print(json.dumps({"cfg": cfg, "n": n, "seed": seed + SEED_BASE, "ran_per_rank": [x["ran"] for x in res],
+                      "nfail": sum(x["nfail"] for x in res)}), flush=True)  # shown with -s
     assert all(x["nfail"] == 0 and x["ran"] >= 100 for x in res), [x for x in res if x["nfail"]][:2]
