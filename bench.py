@@ -299,6 +299,22 @@ def bench_local(args):
     print(json.dumps(res), flush=True)
 
 
+class _StdoutToStderr:
+    """Gloo prints its connection notes ("[Gloo] Rank 0 is connected to ...")
+    on file descriptor 1 while a process group forms; they go to stderr so
+    that rank 0's stdout holds only the one JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def bench_allreduce(args):
     import ctypes
 
@@ -313,7 +329,9 @@ def bench_allreduce(args):
     n = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", rank)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    dist.init_process_group("gloo", rank=rank, world_size=n)
+    with _StdoutToStderr():
+        dist.init_process_group("gloo", rank=rank, world_size=n)
+        dist.barrier()  # every connection made (and noted) inside
     comm = MPI.Init()
     dev = torch.device(f"cuda:{local}")
     stream = torch.cuda.current_stream(dev)
@@ -541,7 +559,8 @@ def bench_allreduce(args):
             rccl["skipped"] = "ranks share one GPU (RCCL needs one GPU per rank)"
         else:
             try:
-                ng = dist.new_group(backend="nccl")
+                with _StdoutToStderr():
+                    ng = dist.new_group(backend="nccl")
                 for nb in sizes:
                     tw, _ = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2,
                                     fn=lambda s_, r_: (r_.copy_(s_), dist.all_reduce(r_, group=ng)))
