@@ -113,6 +113,21 @@ def cpu_reference_allreduce(ranks=8, mib=256, iters=3):
             "kind": "reference", "impl": "MPICH 3.3.2 MPI_Allreduce f32 SUM, host buffers", **host_cpu()}
 
 
+def cpu_baseline_from_allreduce(cpu_ar):
+    """The N > 1 line's cpu_baseline: the reference path itself — MPICH 3.3.2
+    MPI_Allreduce(f32 SUM) of the same per-rank size over 8 ranks on this
+    box's host cores (the call behind /root/reference/src/collective.jl:
+    698-700), measured in the same run (cpu_reference_allreduce), as busbw in
+    the headline's unit.  None when that run failed or was skipped."""
+    if not cpu_ar or "busbw_GBps" not in cpu_ar:
+        return None
+    return {"value": round(cpu_ar["busbw_GBps"], 3), "unit": "GB/s (busbw)", "cores": cpu_ar["cores"],
+            "kind": "reference", "model": cpu_ar.get("model", ""),
+            "sample": f"MPICH 3.3.2 MPI_Allreduce f32 SUM, {cpu_ar['mib']} MiB per rank, {cpu_ar['ranks']} ranks "
+                      f"(mpiexec) on the host cores, {cpu_ar['iters']} timed calls, host buffers, full workload",
+            "sec_per_step": cpu_ar["sec_per_call"], "algbw_GBps": cpu_ar.get("algbw_GBps")}
+
+
 def traffic_from_profiles(key):
     """(per-launch HBM bytes, file) from the newest committed PMC pass
     (profiles/r<NN>*_traffic.json, tools/profile.sh: rocprofv3 cannot run
@@ -142,17 +157,24 @@ def coll_hbm_bytes(kind, n, S):
 
 def coll_traffic_from_profiles(kind, n, mib):
     """(HBM bytes of one call, all ranks, file) from the newest committed
-    collective-kernel PMC profile (profiles/*_coll_n<n>_1gpu.json, tools/coll_prof.py)."""
+    collective-kernel PMC profile (profiles/r<NN>*_coll_n<n>_1gpu*.json,
+    tools/coll_prof.py, whatever its suffix: _xdev_fullgrid etc.).  Files
+    sort by their round prefix; the last one holding this (size, variant)
+    wins."""
     import glob
     best, src = None, None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_coll_n{n}_1gpu.json"))):
+    files = glob.glob(os.path.join(ROOT, "profiles", f"*_coll_n{n}_1gpu*.json"))
+    for f in sorted(files, key=os.path.basename):
         try:
             t = json.load(open(f))["configs"].get(f"{mib}:{kind}", {}).get("traffic") or {}
         except Exception:
             continue
         for k, v in t.items():
-            if "ar_zc_kernel" in k:
-                best, src = v["hbm_bytes_rank0"] * n, os.path.relpath(f, ROOT)
+            # rank 0's kernel HBM bytes (round 4's key; tools/coll_prof.py
+            # names it hbm_bytes_device since round 5)
+            b = v.get("hbm_bytes_rank0", v.get("hbm_bytes_device"))
+            if "ar_zc_kernel" in k and b:
+                best, src = b * n, os.path.relpath(f, ROOT)
     return best, src
 
 
@@ -196,7 +218,26 @@ def bench_local(args):
         torch.cuda.synchronize()
         return a.elapsed_time(b) / reps
 
-    read_ms = [read_probe_ms()] if len(ins) in (1, 2, 4, 8) else []
+    # the fold's own mix: the same 8 reads plus the
+    # 256 MiB of write-through stores, XOR in place of the fold
+    # (mpigx_mix_probe, copy.hip mix_probe_kernel) — the ceiling that is
+    # this kernel's own; the read-only rate stays beside it
+    def mix_probe_ms(reps=10):
+        L = MPI.lib()
+        for _ in range(2):
+            MPI.api._check(L.mpigx_mix_probe(in_ptrs, len(ins), S, ctypes.c_void_p(out.data_ptr()),
+                                             ctypes.c_void_p(stream.cuda_stream)))
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            L.mpigx_mix_probe(in_ptrs, len(ins), S, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
+
+    probes = len(ins) in (1, 2, 4, 8)
+    read_ms = [read_probe_ms()] if probes else []
+    mix_ms = [mix_probe_ms()] if probes else []
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -215,9 +256,11 @@ def bench_local(args):
     algo = (args.nbuf + 1) * S
     if read_ms:
         read_ms.append(read_probe_ms())
-    # the box's read rate: the faster of the two probes (before / after the timed steps)
-    peak_measured = (args.nbuf * S) / (min(read_ms) / 1e3) / 1e9 if read_ms else None
+        mix_ms.append(mix_probe_ms())
 
+    # parity spot check (the probes above wrote `out`: one more fold first)
+    step()
+    torch.cuda.synchronize()
     # parity spot check of the timed output vs the MPICH-pinned oracle (1 Mi elements)
     import numpy as np
     from oracle import mpich_model as M
@@ -267,36 +310,59 @@ def bench_local(args):
     sweep[f"{args.mib}MiB"] = {"GBps": round(algo / (kern_ms / 1e3) / 1e9, 1), "us": round(kern_ms * 1e3, 2)}
     cpu_ar = None if args.no_cpu_baseline else cpu_reference_allreduce()
 
-    achieved = algo / (kern_ms / 1e3) / 1e9
-    value = algo / wall / 1e9
     traffic, traffic_src = traffic_from_profiles("reduce_local_multi_f32_sum_8x256MiB")
-    res = {
+    print(json.dumps(build_local_line({
+        "nbuf": args.nbuf, "mib": args.mib, "steps": args.steps, "warmup": args.warmup, "wall_s": wall,
+        "kern_ms": kern_ms, "read_ms": read_ms, "mix_ms": mix_ms, "parity": parity, "variants": variants,
+        "sweep": sweep, "cpu": cpu, "cpu_ar": cpu_ar, "traffic": traffic, "traffic_src": traffic_src})), flush=True)
+
+
+def build_local_line(m):
+    """The N = 1 JSON line from the measured sections (m: bench_local's
+    numbers; tests/test_bench_line_cpu.py builds it from recorded ones)."""
+    S = m["mib"] << 20
+    algo = (m["nbuf"] + 1) * S
+    achieved = algo / (m["kern_ms"] / 1e3) / 1e9
+    value = algo / m["wall_s"] / 1e9
+    # the box's ceilings: the faster of the two probes of each kind (before /
+    # after the timed steps).  peak_measured = the 8-read : 1-write mix
+    # probe, the fold's own traffic with no fold; the read-only stream beside it
+    mix = algo / (min(m["mix_ms"]) / 1e3) / 1e9 if m.get("mix_ms") else None
+    rd = (m["nbuf"] * S) / (min(m["read_ms"]) / 1e3) / 1e9 if m.get("read_ms") else None
+    return {
         "metric": "Allreduce! busbw GB/s (256MiB f32 SUM) at 1/2/4/8 GPUs; % of xGMI/HBM peak",
-        "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(wall * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": m["steps"], "warmup": m["warmup"],
+        "ms_per_step": round(m["wall_s"] * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32", "data": "synthetic (uniform[-1,1) f32, seeded, resident in HBM)",
-        "config": {"workload": f"config 2: 1xMI355X local MPI.Op kernel, reduce {args.nbuf} rank buffers of "
-                               f"{args.mib} MiB f32 SUM (MPICH association) -> 1 output",
-                   "parallelism": "single GPU", "nbuf": args.nbuf, "bytes_per_buffer": S,
+        "config": {"workload": f"config 2: 1xMI355X local MPI.Op kernel, reduce {m['nbuf']} rank buffers of "
+                               f"{m['mib']} MiB f32 SUM (MPICH association) -> 1 output",
+                   "parallelism": "single GPU", "nbuf": m["nbuf"], "bytes_per_buffer": S,
                    "algorithmic_bytes_per_step": algo},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "peak_measured": round(peak_measured, 1) if peak_measured else None,
-                     "frac_vs_measured": round(achieved / peak_measured, 4) if peak_measured else None,
-                     "peak_measured_basis": "this box's read-only stream of the same 8 inputs in the fold's access "
-                                            "layout (mpigx_read_probe: 8 x 256 MiB read, nothing written), HIP events, "
-                                            "faster of one probe before and one after the timed steps",
-                     "kernel": "fold_local_kernel<OpSum,float,NMAX 8,TREE,SH_FULL,U 4>", "kernel_ms": round(kern_ms, 4),
-                     "achieved_basis": "9 x 256 MiB algorithmic bytes / (HIP-event time over the K timed launches on the launch stream / K)",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": m["traffic"],
+                     "peak_measured": round(mix, 1) if mix else None,
+                     "frac_vs_measured": round(achieved / mix, 4) if mix else None,
+                     "peak_measured_basis": "this box's 8-read : 1-write stream in the fold's layout and store "
+                                            "policy (mpigx_mix_probe: the 8 x 256 MiB inputs read, their XOR "
+                                            "written to the 256 MiB output with the fold's write-through stores, "
+                                            "9 x 256 MiB counted), HIP events, faster of one probe before and one "
+                                            "after the timed steps",
+                     "peak_read_only": round(rd, 1) if rd else None,
+                     "frac_vs_read_only": round(achieved / rd, 4) if rd else None,
+                     "peak_read_only_basis": "mpigx_read_probe: the same 8 inputs read, nothing written (8 x 256 MiB "
+                                             "counted)",
+                     "kernel": "fold_local_kernel<OpSum,float,NMAX 8,TREE,SH_FULL,U 4>",
+                     "kernel_ms": round(m["kern_ms"], 4),
+                     "achieved_basis": "9 x 256 MiB algorithmic bytes / (HIP-event time over the K timed launches on "
+                                       "the launch stream / K)",
                      "traffic_basis": "rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE per dispatch (gfx950 FETCH_SIZE "
-                                      f"halving, MI355X_MICROARCH.md), {traffic_src}"},
-        "cpu_baseline": cpu,
-        "parity_sample_bit_exact": parity,
-        "variants": variants,
-        "sweep_local_f32_sum": sweep,
-        "cpu_reference_allreduce_256MiB": cpu_ar,
+                                      f"halving, MI355X_MICROARCH.md), {m['traffic_src']}"},
+        "cpu_baseline": m["cpu"],
+        "parity_sample_bit_exact": m["parity"],
+        "variants": m["variants"],
+        "sweep_local_f32_sum": m["sweep"],
+        "cpu_reference_allreduce_256MiB": m["cpu_ar"],
     }
-    print(json.dumps(res), flush=True)
 
 
 class _StdoutToStderr:
@@ -731,61 +797,84 @@ def bench_allreduce(args):
             cpu_ar = cpu_reference_allreduce(8, args.mib, 3)
         dist.barrier()
 
+    if rank == 0:
+        kind = {"pull-push two-shot": "pullpush", "push two-shot": "push"}.get(ar_tune["choice"], "pull")
+        traffic, traffic_src = coll_traffic_from_profiles(kind, n, args.mib) if same_device else (None, None)
+        print(json.dumps(build_coll_line({
+            "n": n, "mib": args.mib, "steps": args.steps, "warmup": args.warmup, "t": t, "kern": kern,
+            "same_device": same_device, "ar_tune": ar_tune, "traffic": traffic, "traffic_src": traffic_src,
+            "xg": xg, "cpu_ar": cpu_ar, "correct": correct, "tune_classes": tune_classes, "probe": probe,
+            "phases": phases, "section_s": section_s, "sweep": sweep, "rccl": rccl, "cfg4": cfg4,
+            "tune_classes4": tune_classes4, "cfg5": cfg5, "cfg5_ok": cfg5_ok[0] and "config5" not in errors,
+            "errors": errors})), flush=True)
+    try:
+        MPI.Finalize()
+    finally:
+        dist.destroy_process_group()
+
+
+def build_coll_line(m):
+    """The N > 1 JSON line from the measured sections (m: bench_allreduce's
+    numbers; tests/test_bench_line_cpu.py builds it from recorded ones)."""
+    n, S, t, kern = m["n"], m["mib"] << 20, m["t"], m["kern"]
+
+    def busbw(nbytes, tt):
+        return nbytes / tt * 2 * (n - 1) / n / 1e9
+
     value = busbw(S, t)
     ach = busbw(S, kern)
     peak_nom = XGMI_LINK_GBPS * (n - 1)
-    if same_device:
+    xg = m["xg"]
+    if m["same_device"]:
         # every rank's kernel streams the same HBM: achieved = the chosen
         # variant's algorithmic HBM bytes of one call, all ranks, / device time
-        kind = {"pull-push two-shot": "pullpush", "push two-shot": "push"}.get(ar_tune["choice"], "pull")
+        kind = {"pull-push two-shot": "pullpush", "push two-shot": "push"}.get(m["ar_tune"]["choice"], "pull")
         hbm_b = coll_hbm_bytes(kind, n, S)
-        traffic, traffic_src = coll_traffic_from_profiles(kind, n, args.mib)
         roof = {"bound": "hbm (same-device IPC)", "achieved": round(hbm_b / kern / 1e9, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(hbm_b / kern / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "unit": "GB/s", "frac": round(hbm_b / kern / 1e9 / HBM_PEAK_GBPS, 4), "traffic": m["traffic"],
                 "kernel": f"ar_zc_kernel ({kind})", "algorithmic_hbm_bytes_per_call": hbm_b,
                 "busbw_device_GBps": round(ach, 1),
-                "traffic_basis": f"rocprofv3 PMC of rank 0's kernel x {n} ranks, {traffic_src}" if traffic_src else None,
+                "traffic_basis": f"rocprofv3 PMC of rank 0's kernel x {n} ranks, {m['traffic_src']}"
+                if m["traffic_src"] else None,
                 "note": "all ranks share one GPU: peer pulls / pushes are HBM accesses through IPC mappings, no xGMI"}
     else:
         roof = {"bound": "xgmi", "achieved": round(ach, 1), "peak": round(peak_nom, 1), "unit": "GB/s",
                 "frac": round(ach / peak_nom, 4),
                 "traffic": xg["read_bytes_per_step"] if xg else None,
                 "peak_basis": f"nominal {n - 1} links x {XGMI_LINK_GBPS} GB/s per direction (MI355X spec)"}
-    roof.update({"achieved_basis": ("algorithmic HBM bytes of one call (all ranks) / " if same_device else "busbw of ")
+    roof.update({"achieved_basis": ("algorithmic HBM bytes of one call (all ranks) / " if m["same_device"] else
+                                    "busbw of ")
                  + "the blocking call's device time (HIP events around each call on the comm stream), max over ranks",
                  "xgmi_traffic": xg})
-    if rank == 0:
-        res = {
-            "metric": "Allreduce! busbw GB/s (256MiB f32 SUM) at 1/2/4/8 GPUs; % of xGMI/HBM peak",
-            "value": round(value, 2), "unit": "GB/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(t * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32", "data": "synthetic (uniform[-1,1) f32 per rank, seeded, resident in HBM)",
-            "config": {"workload": f"config 3 at {args.mib} MiB: MPI.Allreduce!(SUM) f32, blocking, {n} ranks",
-                       "parallelism": f"{n} ranks x 1 GPU (hipIpc peer-mapped HBM over xGMI)"
-                       if not same_device else f"{n} ranks sharing one GPU (same-device IPC)",
-                       "bytes_per_rank": S, "algbw_GBps": round(S / t / 1e9, 2), "same_device_ranks": same_device},
-            "roofline": roof,
-            "cpu_baseline": None,
-            "cpu_reference_allreduce": cpu_ar,
-            "correct": correct,
-            "ar_tune": ar_tune,
-            "tune_classes": tune_classes,
-            "xgmi_probe_informational": dict(probe, note="engine's own all-peer / one-link pull of 64 MiB; not a "
-                                                         "peak (it measured below the collective at n=3 in r02)"),
-            "phases_headline_us": phases,
-            "section_wall_s": section_s,
-            "sweep_mpigx_busbw": sweep,
-            "rccl_busbw": rccl,
-            "config4_bcast_allgather_alltoall": cfg4,
-            "tune_classes_after_config4": tune_classes4,
-            "config5_scan_exscan_reduce": {"bit_exact_all": cfg5_ok[0] and "config5" not in errors, "cases": cfg5},
-            "errors": errors or None,
-        }
-        print(json.dumps(res), flush=True)
-    try:
-        MPI.Finalize()
-    finally:
-        dist.destroy_process_group()
+    return {
+        "metric": "Allreduce! busbw GB/s (256MiB f32 SUM) at 1/2/4/8 GPUs; % of xGMI/HBM peak",
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": n, "steps": m["steps"], "warmup": m["warmup"],
+        "ms_per_step": round(t * 1e3, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic (uniform[-1,1) f32 per rank, seeded, resident in HBM)",
+        "config": {"workload": f"config 3 at {m['mib']} MiB: MPI.Allreduce!(SUM) f32, blocking, {n} ranks",
+                   "parallelism": f"{n} ranks x 1 GPU (hipIpc peer-mapped HBM over xGMI)"
+                   if not m["same_device"] else f"{n} ranks sharing one GPU (same-device IPC)",
+                   "bytes_per_rank": S, "algbw_GBps": round(S / t / 1e9, 2), "same_device_ranks": m["same_device"]},
+        "roofline": roof,
+        # the reference path itself on this box's host cores, same run
+        # (VERDICT r05 item 1): MPICH MPI_Allreduce, 8 ranks, same size
+        "cpu_baseline": cpu_baseline_from_allreduce(m["cpu_ar"]),
+        "cpu_reference_allreduce": m["cpu_ar"],
+        "correct": m["correct"],
+        "ar_tune": m["ar_tune"],
+        "tune_classes": m["tune_classes"],
+        "xgmi_probe_informational": dict(m["probe"] or {}, note="engine's own all-peer / one-link pull of 64 MiB; "
+                                                                "not a peak (it measured below the collective at n=3 "
+                                                                "in r02)"),
+        "phases_headline_us": m["phases"],
+        "section_wall_s": m["section_s"],
+        "sweep_mpigx_busbw": m["sweep"],
+        "rccl_busbw": m["rccl"],
+        "config4_bcast_allgather_alltoall": m["cfg4"],
+        "tune_classes_after_config4": m["tune_classes4"],
+        "config5_scan_exscan_reduce": {"bit_exact_all": m["cfg5_ok"], "cases": m["cfg5"]},
+        "errors": m["errors"] or None,
+    }
 
 
 def _ring_check(M, np, recv, count, n, rank_input, tmax, nch):

@@ -58,6 +58,13 @@ int mpigx_comm_diag_break(mpigx_comm_t comm);
  * buffer of >= 4 KiB that is never written in practice.  Enqueued on
  * `stream` (hipStream_t; NULL = null stream), asynchronous. */
 int mpigx_read_probe(const void *const *in, int nin, long long bytes, void *sink, void *stream);
+/* The same stream with the fold's writes put back: reads the `nin` inputs in
+ * the fold's layout and stores, per 16-B vector, the XOR of the nin loaded
+ * vectors into `out` (`bytes` bytes, 16-B aligned) with the fold's
+ * write-through stores — config 2's read/write mix (8 reads : 1 write) with
+ * no arithmetic to speak of: the box's ceiling for that kernel
+ * (roofline.peak_measured in bench.py).  Asynchronous on `stream`. */
+int mpigx_mix_probe(const void *const *in, int nin, long long bytes, void *out, void *stream);
 /* Zero-copy paths (user buffers mapped by the peers over IPC): how many
  * launches ran on a cached view without any host exchange, and how many
  * host exchanges of buffer registrations there were.  Diagnostic. */

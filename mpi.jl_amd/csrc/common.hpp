@@ -51,15 +51,26 @@ enum Shape : int { SH_PRE = 0, SH_POW2 = 1, SH_FULL = 2 };
 constexpr int AG_PULL = 0, AG_PUSH = 1;
 
 // The local fold's shape and 16-B vectors per thread — ONE rule for the host
-// (grid size) and the launcher (instantiation).  SH_FULL only at NMAX 8 (the
-// 8-buffer headline; n = 16 takes SH_POW2).  U = 4 measured best or tied on
-// three MI355X boxes (tools/fold_tune.hip, profiles/r02_fold_tune*.json);
-// bf16 MIN/MAX keep U = 1 (their owner-dispatched trees need the VGPRs).
+// (grid size, FoldArgs.lu) and the launcher (instantiation).  SH_FULL only at
+// NMAX 8 (the 8-buffer headline; n = 16 takes SH_POW2).  U = 4 measured best
+// or tied on three MI355X boxes at 256 MiB (tools/fold_tune.hip,
+// profiles/r02_fold_tune*.json); bf16 MIN/MAX keep U = 1 (their
+// owner-dispatched trees need the VGPRs).
 constexpr int fold_shape(int sched, int nmax, int ntree, int rem) {
   return (sched == 0 && rem > 0) ? SH_PRE : (nmax == 8 && ntree == 8) ? SH_FULL : SH_POW2;
 }
-constexpr int local_u(int rep, int op, int shape) {
+constexpr int local_u_max(int rep, int op, int shape) {
   return shape != SH_FULL ? 1 : (rep == R_BF16 && (op == O_MIN || op == O_MAX)) ? 1 : 4;
+}
+// ... and by size: at U = 4 a 1 MiB input made 64
+// blocks of 256 threads, a quarter of the CUs.  U halves until the one-pass
+// grid has at least kLocalMinBlocks blocks (or U is 1): U = 4 from 1 Mi
+// 16-B vectors per input (16 MiB), 2 from 512 Ki, 1 below.
+constexpr long long kLocalMinBlocks = 1024;
+constexpr int local_u(int rep, int op, int shape, long long nvec) {
+  int u = local_u_max(rep, op, shape);
+  while (u > 1 && nvec < (long long)u * kThreads * kLocalMinBlocks) u /= 2;
+  return u;
 }
 
 // Fold schedule (template parameter of the fold kernels).
@@ -158,15 +169,18 @@ struct PeerView {
   uint64_t* sig_uc;            // my uncached signal array (cross-device writers)
   uint64_t* sig_rw;            // my cached signal array (same-device writers and myself)
   const char* ll_rw;           // my cached LL area at this launch's parity (same-device senders)
-  // Waiting for a late peer (round 5, DESIGN §3 "a late rank"): a blocking
-  // call's host watches its peers while it waits (mpigx.cpp finish), so its
-  // kernel's polls never give up on time alone — they give up when the host
-  // stores a nonzero `cancel` word (a peer's process is gone, its
-  // communicator failed, or every rank's kernel has been stuck past the
-  // timeout).  Stream-ordered launches (nobody watching: cancel = null) keep
-  // the timeout.  Block 0 stores `kseq` (this launch's number, the same on
-  // every rank) into `started` at entry, which tells the host — and through
-  // the shm block its peers — which launch its GPU is in.
+  // Waiting for a late peer (round 5, DESIGN §3 "a late rank"): every
+  // launch's polls give up only when its host stores a nonzero `cancel` word
+  // (make_view sets it for every launch), never on time alone.  A blocking
+  // call's host watches its peers while it waits (mpigx.cpp finish); a
+  // stream-ordered launch's peers are watched by the process-wide watcher
+  // (watch_peers).  Either cancels when a peer's process is gone, its
+  // communicator failed, a peer's launch is stuck behind other communicators'
+  // kernels (never started although enqueued), or — blocking calls — every
+  // rank's kernel has sat in the launch past the timeout.  Block 0 stores
+  // `kseq` (this launch's number, the same on every rank) into `started` at
+  // entry, which tells the host — and through the shm block its peers —
+  // which launch its GPU is in.
   unsigned long long kseq;
   unsigned long long* started;
   const unsigned* cancel;
@@ -237,6 +251,7 @@ struct FoldArgs {
   // end (the agreed view's exported sizes): the remote stores are checked
   // against them before any is made
   long long zc_avail[kMaxRanks];
+  int lu;              // M_LOCAL: 16-B vectors per thread the host sized the grid for (local_u)
 };
 
 // Ring reduce-scatter + allgather (MPIGX_ALGO=ring; kernels.hpp ring_kernel).

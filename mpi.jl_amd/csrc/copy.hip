@@ -144,6 +144,7 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
     __syncthreads();  // IN_PLACE Alltoall: this slice of my blocks is read before peers' bytes land on it
     bool ok = true;
     const uint64_t t0 = wall_clock64();
+    uint64_t next = kCancelPoll;  // one cancel-word read per kCancelPoll of waiting
     for (int p = 0; p < n && ok; ++p) {
       if (p == r) continue;
       const char* in = ll_from(pv, A.ll_in, p, A.ll_stride);
@@ -151,11 +152,11 @@ __device__ __forceinline__ int copy_body(const CopyArgs& A) {  // returns the ze
       if (!bc || p == A.root) {
         char* dst = bc ? recv : recv + (long long)p * A.total;
         for (long long i = l0 + tid; i < l1 && ok; i += nt) {
-          ok = ll_get(pv, in, i, flag, t0, &d);
+          ok = ll_get(pv, in, i, flag, t0, next, &d);
           if (ok) ll_store8(dst, i, A.bytes, d);
         }
       } else if (b == 0 && tid == 0) {
-        ok = ll_get(pv, in, 0, flag, t0, &d);
+        ok = ll_get(pv, in, 0, flag, t0, next, &d);
       }
     }
     if (!ok) __hip_atomic_store(pv.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -564,6 +565,73 @@ hipError_t launch_read_probe(const void* const* in, int nin, long long bytes, vo
     case 2: hipLaunchKernelGGL(read_probe_kernel<2>, grid, dim3(kThreads), 0, s, a); break;
     case 4: hipLaunchKernelGGL(read_probe_kernel<4>, grid, dim3(kThreads), 0, s, a); break;
     case 8: hipLaunchKernelGGL(read_probe_kernel<8>, grid, dim3(kThreads), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// 8-read : 1-write stream (mpigx_diag.h mpigx_mix_probe): config 2's own
+// ceiling on the box it runs on.  The read probe above
+// measures the inputs alone; the fold also writes 256 MiB, and the box's rate
+// for that mix is what bounds it.  Same layout, loads and stores as
+// fold_local_kernel<SH_FULL, U = 4>: thread t of block b loads the four 16-B
+// vectors (4b+u)*256 + t of every input (all nin x 4 loads in flight first),
+// then stores, per vector, the XOR of its nin loads with the fold's
+// write-through buffer store (stv_wt).  XOR is one VALU op per dword, so what
+// is left of the fold is its memory traffic and its load -> store dependence.
+// ---------------------------------------------------------------------------
+struct MixProbeArgs {
+  const char* in[kMaxRanks];
+  long long nvec;  // 16-B vectors per input (and of the output)
+  char* out;
+};
+template <int NIN>
+__global__ __launch_bounds__(kThreads) void mix_probe_kernel(MixProbeArgs A) {
+  constexpr int U = 4;
+  const long long tid = threadIdx.x;
+  const long long step = (long long)gridDim.x * (U * kThreads);
+  for (long long v0 = (long long)blockIdx.x * (U * kThreads) + tid; v0 < A.nvec; v0 += step) {
+    if (v0 + (long long)(U - 1) * kThreads < A.nvec) {
+      u32x4 x[U][NIN];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int s = 0; s < NIN; ++s) x[u][s] = ld16(A.in[s] + 16 * (v0 + (long long)u * kThreads));
+      const __amdgpu_buffer_rsrc_t span = span_rsrc(A.out + 16 * (v0 - tid), U * kThreads * 16);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        Vec<unsigned, 4> r;
+        u32x4 a = x[u][0];
+#pragma unroll
+        for (int s = 1; s < NIN; ++s) a ^= x[u][s];
+        *reinterpret_cast<u32x4*>(r.x) = a;
+        stv_wt<unsigned, 4>(span, (int)(tid + u * kThreads) * 16, r);
+      }
+    } else {
+      for (int u = 0; u < U; ++u) {
+        const long long k = v0 + (long long)u * kThreads;
+        if (k >= A.nvec) break;
+        u32x4 a = ld16(A.in[0] + 16 * k);
+        for (int s = 1; s < NIN; ++s) a ^= ld16(A.in[s] + 16 * k);
+        st16(A.out + 16 * k, a);
+      }
+    }
+  }
+}
+
+hipError_t launch_mix_probe(const void* const* in, int nin, long long bytes, void* out, hipStream_t s) {
+  MixProbeArgs a;
+  for (int k = 0; k < kMaxRanks; ++k) a.in[k] = k < nin ? (const char*)in[k] : nullptr;
+  a.nvec = bytes / 16;
+  a.out = (char*)out;
+  const long long g = (a.nvec + 4 * kThreads - 1) / (4 * kThreads);
+  const dim3 grid((unsigned)(g < 1 ? 1 : g > (1ll << 30) ? (1ll << 30) : g));
+  switch (nin) {
+    case 1: hipLaunchKernelGGL(mix_probe_kernel<1>, grid, dim3(kThreads), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(mix_probe_kernel<2>, grid, dim3(kThreads), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(mix_probe_kernel<4>, grid, dim3(kThreads), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(mix_probe_kernel<8>, grid, dim3(kThreads), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -903,11 +903,14 @@ __device__ __forceinline__ void spin_pause(unsigned& k) {
   ++k;
 }
 
-// When a poll loop gives up (PeerView.cancel): a stream-ordered launch after
-// timeout_ticks; a blocking one only when its host stores the cancel word
-// (read once per kCancelPoll of waiting — a PCIe read of a host-pinned word —
-// so a late peer is waited for as long as its host says it is coming).  A
-// zero timeout (a failed host gate) gives up at once either way.
+// When a poll loop gives up (PeerView.cancel): only when its host stores the
+// cancel word — every launch, blocking or stream-ordered, carries it
+// (mpigx.cpp make_view): a blocking call's host stores it from finish(), a
+// stream-ordered launch's from the process-wide watcher (watch_peers).  The
+// word is read once per kCancelPoll of waiting (a PCIe read of a host-pinned
+// word), so a late peer is waited for as long as its host says it is coming.
+// A zero timeout (a failed host gate) gives up at once; a view without a
+// cancel word (none is built today) would fall back to timeout_ticks.
 constexpr uint64_t kCancelPoll = 100000;  // 1 ms of the 100 MHz wall clock
 __device__ __forceinline__ bool spin_expired(const PeerView& pv, uint64_t t0, uint64_t& next) {
   const uint64_t el = wall_clock64() - t0;
@@ -1166,12 +1169,14 @@ __device__ __forceinline__ void ll_put(char* area, long long i, uint64_t d, unsi
   __hip_atomic_store(q + 1, (d >> 32) | fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // waits for line i of a sender's area to carry `flag`; false when the wait
-// gives up (spin_expired; t0 = the start of the caller's wait)
+// gives up (spin_expired; t0 = the start of the caller's wait, `next` its
+// deadline for the next cancel-word read, kept across the caller's lines so
+// the host-pinned word is read at most once per kCancelPoll, not at the first
+// miss of every line once the wait has passed 1 ms)
 __device__ __forceinline__ bool ll_get(const PeerView& pv, const char* area, long long i, unsigned flag, uint64_t t0,
-                                       uint64_t* d) {
+                                       uint64_t& next, uint64_t* d) {
   const uint64_t* q = reinterpret_cast<const uint64_t*>(area + kLLLine * i);
   unsigned k = 0;
-  uint64_t next = kCancelPoll;
   for (;;) {
     const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1237,11 +1242,12 @@ __device__ __noinline__ bool ll_exchange(const PeerView& pv, char* const* push, 
   flush_remote_stores();
   bool ok = true;
   const uint64_t t0 = wall_clock64();
+  uint64_t next = kCancelPoll;  // one cancel-word read per kCancelPoll of waiting (ll_get)
   for (long long i = l0 + tid; i < l1 && ok; i += nt) {
     for (int p = 0; p < n && ok; ++p) {
       if (p == r) continue;
       const uint64_t* q = reinterpret_cast<const uint64_t*>(ll_from(pv, in, p, stride) + kLLLine * i);
-      uint64_t a, b, next = kCancelPoll;
+      uint64_t a, b;
       unsigned k = 0;
       for (;;) {
         a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -55,23 +55,41 @@ template <> struct OpOf<O_BXOR> { using type = OpBxor; };
 template <> struct OpOf<O_REPLACE> { using type = OpReplace; };
 template <> struct OpOf<O_NOOP> { using type = OpNoop; };
 
+// SH_FULL local fold at the U the host chose (local_u: UF at large sizes,
+// halved for small inputs)
+template <class OP, int SCHED, int UF>
+void local_full(int lu, dim3 grid, hipStream_t s, const FoldArgs& a) {
+  if constexpr (UF >= 4) {
+    if (lu >= 4) {
+      hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, SCHED, SH_FULL, 4>), grid, dim3(kThreads), 0, s, a);
+      return;
+    }
+    if (lu == 2) {
+      hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, SCHED, SH_FULL, 2>), grid, dim3(kThreads), 0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, SCHED, SH_FULL, 1>), grid, dim3(kThreads), 0, s, a);
+}
+
 template <class OP>
 hipError_t fold_op(int nmax, int sched, dim3 grid, hipStream_t s, const FoldArgs& a) {
   if (a.mode == M_LOCAL) {
     // shape and vectors per thread: fold_shape / local_u (common.hpp), the
-    // rule the host sized the grid with
-    constexpr int UF = local_u(MPIGX_REP, OP::code, SH_FULL);
+    // rule the host sized the grid with (a.lu); the kernel is correct for any
+    // grid, U only sets how much of the range one pass covers
+    constexpr int UF = local_u_max(MPIGX_REP, OP::code, SH_FULL);
     const int shape = fold_shape(sched, nmax, a.ntree, a.rem);
     if (sched == S_LINEAR) {
       if (nmax > 8)
         hipLaunchKernelGGL((fold_local_kernel<OP, T, 16, S_LINEAR, SH_POW2, 1>), grid, dim3(kThreads), 0, s, a);
       else if (shape == SH_FULL)
-        hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_LINEAR, SH_FULL, UF>), grid, dim3(kThreads), 0, s, a);
+        local_full<OP, S_LINEAR, UF>(a.lu, grid, s, a);
       else
         hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_LINEAR, SH_POW2, 1>), grid, dim3(kThreads), 0, s, a);
     } else if (nmax <= 8) {
       if (shape == SH_FULL)
-        hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_TREE, SH_FULL, UF>), grid, dim3(kThreads), 0, s, a);
+        local_full<OP, S_TREE, UF>(a.lu, grid, s, a);
       else if (shape == SH_POW2)
         hipLaunchKernelGGL((fold_local_kernel<OP, T, 8, S_TREE, SH_POW2, 1>), grid, dim3(kThreads), 0, s, a);
       else

@@ -369,6 +369,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
     const unsigned flag = A.ll_flag;
     const long long half = A.ll_stride / 2;
     const uint64_t t0 = wall_clock64();
+    uint64_t next = kCancelPoll;  // one cancel-word read per kCancelPoll of waiting
     bool ok = true;
     // chunk c: element offset, bytes, and this block's line range
     long long lo, hi;  // this block's elements of the chunk (chunk-relative)
@@ -396,7 +397,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       if (p == r) continue;
       for (long long i = rl0 + tid; i < rl1 && ok; i += nt) {
         uint64_t d;
-        ok = ll_get(pv, ll_from(pv, A.ll_in, p, A.ll_stride), i, flag, t0, &d);
+        ok = ll_get(pv, ll_from(pv, A.ll_in, p, A.ll_stride), i, flag, t0, next, &d);
         if (ok) *reinterpret_cast<uint64_t*>((char*)mine + (long long)p * A.slot_bytes + 8 * i) = d;
       }
     }
@@ -427,7 +428,7 @@ __device__ __forceinline__ int fold_body(const FoldArgs& A) {  // returns the ze
       span(p, &c0, &cb, &l0, &l1);
       for (long long i = l0 + tid; i < l1 && ok; i += nt) {
         uint64_t d;
-        ok = ll_get(pv, ll_from(pv, A.ll_in, p, A.ll_stride) + half, i, flag, t0, &d);
+        ok = ll_get(pv, ll_from(pv, A.ll_in, p, A.ll_stride) + half, i, flag, t0, next, &d);
         if (ok) ll_store8((char*)recv + c0 * es, i, cb, d);
       }
     }

@@ -52,5 +52,6 @@ hipError_t launch_pack(hipStream_t s, const PackArgs& a);
 // read-only stream of nin (1, 2, 4, 8) buffers of `bytes` each (copy.hip; the
 // per-box ceiling of config 2)
 hipError_t launch_read_probe(const void* const* in, int nin, long long bytes, void* sink, hipStream_t s);
+hipError_t launch_mix_probe(const void* const* in, int nin, long long bytes, void* out, hipStream_t s);
 
 }  // namespace mpigx

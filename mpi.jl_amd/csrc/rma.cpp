@@ -291,11 +291,22 @@ int post(mpigx_win* w, int t, int kind, int op, int rep, long long tdisp, long l
   if (needs_src && !same_process(c, t) &&
       !rt::export_buf(c, origin, &tmp.buf_id, &tmp.off, &tmp.h))
     return MPIGX_ERR_BUFFER;
-  const uint64_t seq = w->sseq[t];
+  // Claim the sequence number before anything can yield the big lock
+  // (spin_progress): under THREAD_MULTIPLE another thread's Put to the same
+  // target may post while this one waits for its slot, and reading sseq
+  // before the wait and advancing it after let two threads fill one
+  // envelope.  Claimed numbers are posted in any order; the
+  // target applies them in sequence order (rma_progress polls slot rseq).
+  const uint64_t seq = w->sseq[t]++;
   RmaEnvelope* e = &wshm(w)->box[c->rank][t].slot[seq % kRmaSlots];
   Deadline d(c);
-  // the slot is free once its previous envelope (seq - 16) was applied
-  while (e->done.load(std::memory_order_acquire) != e->posted.load(std::memory_order_relaxed)) {
+  // the slot is mine once ITS previous envelope (seq - 16) was posted and
+  // applied — not just any earlier one: with claims outstanding, seq + 16
+  // waits on the same slot and must not take it before seq has used it
+  const uint64_t prev_posted = seq >= (uint64_t)kRmaSlots ? seq + 1 - kRmaSlots : 0;
+  for (;;) {
+    const uint64_t pp = e->posted.load(std::memory_order_acquire);
+    if (pp == prev_posted && e->done.load(std::memory_order_acquire) == pp) break;
     int rc = spin_progress(w, d);
     if (rc) return rc;
   }
@@ -312,7 +323,6 @@ int post(mpigx_win* w, int t, int kind, int op, int rep, long long tdisp, long l
   e->raw = tmp.raw;
   e->h = tmp.h;
   e->posted.store(seq + 1, std::memory_order_release);
-  w->sseq[t] = seq + 1;
   if (seq_out) *seq_out = seq;
   return MPIGX_SUCCESS;
 }

@@ -16,7 +16,7 @@ namespace mpigx {
 // ---------------------------------------------------------------------------
 // shm block (one per communicator, mapped by every rank)
 // ---------------------------------------------------------------------------
-constexpr uint64_t kMagic = 0x6d70696778763035ull;  // "mpigxv05"
+constexpr uint64_t kMagic = 0x6d70696778763036ull;  // "mpigxv06"
 
 constexpr uint64_t kSigCanary = 0x6d70696778c0ffeeull;  // signal-array canary (mpigx.cpp comm_init)
 
@@ -46,10 +46,15 @@ struct ShmRank {
   // waits (mpigx.cpp finish / host_allgather_wait): `broken` = its
   // communicator failed (it will never join another collective), `kseq_enq`
   // = the last collective launch it enqueued, `kseq_run` = the last one its
-  // device reported started (kernels' `started` word)
+  // device reported started (kernels' `started` word), `proc_busy` = how many
+  // communicators of its PROCESS have a collective in flight (this one
+  // included; mpigx.cpp busy_comms) — a launch enqueued long ago that its GPU
+  // never started while other communicators' kernels run is stuck, not late
+  // (mpigx.cpp stuck_peer)
   std::atomic<int> broken;
   std::atomic<uint64_t> kseq_enq;
   std::atomic<uint64_t> kseq_run;
+  std::atomic<int> proc_busy;
   // host control-plane exchange (host_allgather): double-buffered blobs
   std::atomic<uint64_t> xseq;
   char xbuf[2][256];
@@ -186,6 +191,16 @@ struct mpigx_comm {
   volatile unsigned* cancel = nullptr;
   unsigned* cancel_dev = nullptr;
   unsigned long long kseq = 0;  // collective launches so far (the same on every rank)
+  unsigned long long kseq_done = 0;  // launches known complete (kseq when the last finish() returned)
+  // stuck-peer tracking (mpigx.cpp stuck_peer): since when rank q has been
+  // seen enqueued-but-not-started in the awaited launch (0: not seen so)
+  double stuck_since[mpigx::kMaxRanks] = {};
+  // the watcher's view of a stream-ordered communicator: the launch its GPU
+  // last reported started, since when, and whether its stream had work
+  unsigned long long watch_seen = 0;
+  double watch_moved = 0;
+  bool watch_busy = false;
+  hipEvent_t so_ev = nullptr;  // recorded after every stream-ordered launch (note_launch)
   unsigned long long done_target = 0;  // launch sequence the host waits for
   unsigned long long* dcount_dev = nullptr;
   unsigned long long dcount_total = 0;  // blocks counted on dcount so far

@@ -68,6 +68,7 @@ PROTOTYPES = {
     "mpigx_comm_tune_class": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double)]),
     "mpigx_comm_probe": (c_int, [c_void_p, c_int, c_longlong, ctypes.POINTER(ctypes.c_double)]),
     "mpigx_read_probe": (c_int, [ctypes.POINTER(c_void_p), c_int, c_longlong, c_void_p, c_void_p]),
+    "mpigx_mix_probe": (c_int, [ctypes.POINTER(c_void_p), c_int, c_longlong, c_void_p, c_void_p]),
     "mpigx_barrier": (c_int, [c_void_p]),
     "mpigx_bcast": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "mpigx_allgather": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),

@@ -19,6 +19,6 @@ import torch.distributed as dist  # noqa: E402
 objs = [None] * size
 dist.all_gather_object(objs, raw.hex())
 assert len(set(objs)) == 1, objs
-assert raw.startswith(b"/mpigx-") and raw[64:72] == b"50vxgipm"
+assert raw.startswith(b"/mpigx-") and raw[64:72] == b"60vxgipm"
 print("BOOT", rank, raw[:40].decode(errors="replace").rstrip("\x00"), flush=True)
 dist.destroy_process_group()

@@ -10,6 +10,12 @@ watch the peers (mpigx.cpp finish, PeerView.cancel).
   (collective.jl:698-700 blocks until every rank arrives): the call waits for
   it and every rank gets the exact sum.  A second call right after must be
   exact too.
+* late_stream — the last rank is late on its GPU, not on its host: its
+  stream holds 2.5 x MPIGX_TIMEOUT_MS of earlier work (torch.cuda._sleep)
+  when it makes the blocking call, so its host waits in the call from the
+  start while its GPU has not reached the launch.  That rank is the late
+  one and must not declare a protocol stall (its peers are all
+  in the launch, its own GPU is still in the previous one); exact results;
 * late_vx — the same, before an Allgatherv (its rounds are agreed over the
   host control plane before any launch, so the early ranks wait on the host,
   host_allgather);
@@ -81,6 +87,31 @@ def main():
         out["late_call_s"] = round(time.time() - t0, 3)
         if not bool((recv == want).all()):
             fails.append("late call")
+        recv.fill_(-1)
+        MPI.Allreduce_(send, recv, MPI.SUM, comm)
+        if not bool((recv == want).all()):
+            fails.append("call after")
+        MPI.Barrier(comm)
+        MPI.Finalize()
+    elif scenario == "late_stream":
+        # calibrate torch.cuda._sleep (clock cycles) on this box, then queue
+        # 2.5 x the timeout of it on the last rank's stream
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        torch.cuda._sleep(10_000_000)
+        b.record()
+        torch.cuda.synchronize()
+        per_cycle_s = a.elapsed_time(b) / 1e3 / 10_000_000
+        MPI.Barrier(comm)
+        recv.fill_(-1)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        if r == n - 1:
+            torch.cuda._sleep(int(2.5 * timeout_s / per_cycle_s))
+        MPI.Allreduce_(send, recv, MPI.SUM, comm)
+        out["late_call_s"] = round(time.time() - t0, 3)
+        if not bool((recv == want).all()):
+            fails.append("call behind a busy stream")
         recv.fill_(-1)
         MPI.Allreduce_(send, recv, MPI.SUM, comm)
         if not bool((recv == want).all()):

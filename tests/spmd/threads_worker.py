@@ -53,8 +53,74 @@ def exchange(comm, n_msgs, nthreads, tag0):
     return torch.equal(recv_arr, want)
 
 
+def concurrent_comms(comm, size, rank, stuck_mode):
+    """Collectives on distinct communicators from distinct threads at once
+    (each communicator's calls stay ordered, as MPI requires): every thread
+    runs a loop of Allreduce! (LL, one-shot and zero-copy sizes) and Bcast!
+    on its own Comm_dup of COMM_WORLD.  With MPIGX_CONCURRENT_COMMS covering
+    the three communicators every result must be exact.  stuck_mode (the
+    launcher leaves the knob at 1): the three grids need not fit on the GPU
+    together, and a launch stuck behind the other communicators' kernels
+    must end its call with MPI_ERR_OTHER (mpigx.cpp stuck_peer) instead of
+    waiting forever; every thread has to come back either way, and every
+    result that is returned must be exact."""
+    comms = [MPI.Comm_dup(comm) for _ in range(3)]
+    results = [None] * len(comms)
+
+    def loop(i):
+        cm = comms[i]
+        ok = True
+        # each thread on its own stream (the mirror runs a communicator's
+        # collectives on the caller's current stream; two communicators'
+        # kernels queued on ONE stream in different orders on different
+        # ranks would wait for each other — the rule NCCL / RCCL state
+        # for concurrent communicators too)
+        torch.cuda.set_stream(torch.cuda.Stream())
+        try:
+            for rep in range(3 if stuck_mode else 1):
+                for it, cnt in enumerate((7, 1000, 60000, (32 << 20) // 4, 5)):
+                    x = torch.full((cnt,), float(rank + 1 + i), device="cuda")
+                    y = MPI.Allreduce(x, MPI.SUM, cm)
+                    ok &= bool((y == float(sum(q + 1 + i for q in range(size)))).all())
+                    b = torch.full((cnt,), float(it) if rank == 0 else -1.0, device="cuda")
+                    MPI.Bcast_(b, 0, cm)
+                    ok &= bool((b == float(it)).all())
+            torch.cuda.synchronize()
+            results[i] = ok
+        except MPI.MPIError as e:
+            results[i] = f"MPIError {e.code}"
+
+    ths = [threading.Thread(target=loop, args=(i,)) for i in range(len(comms))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(180)
+    alive = any(t.is_alive() for t in ths)
+    if not stuck_mode:
+        check(all(r is True for r in results) and not alive, f"concurrent collectives on {len(comms)} comms: {results}")
+    else:
+        errs = [r for r in results if isinstance(r, str)]
+        check(not alive, f"every thread came back: {results}")
+        check(all(r is True or r == f"MPIError {MPI.consts.MPI_ERR_OTHER}" for r in results), f"results: {results}")
+        print(json.dumps({"rank": rank, "stuck_results": results, "errors": len(errs)}), flush=True)
+    for cm in comms:
+        try:
+            MPI.free(cm)
+        except MPI.MPIError:
+            pass  # a communicator that failed above
+    return results
+
+
 def main():
     provided = MPI.Init_thread(MPI.THREAD_MULTIPLE)       # test_threads.jl:11
+    if os.environ.get("THREADS_MODE") == "stuck":
+        comm = MPI.COMM_WORLD
+        concurrent_comms(comm, MPI.Comm_size(comm), MPI.Comm_rank(comm), stuck_mode=True)
+        MPI.Barrier(comm)
+        MPI.Finalize()
+        print(json.dumps({"rank": MPI.Comm_rank(comm), "provided": provided, "checks": NCHECK[0],
+                          "failures": FAIL[:10], "nfail": len(FAIL)}), flush=True)
+        sys.exit(1 if FAIL else 0)
     check(MPI.THREAD_SINGLE <= provided <= MPI.THREAD_MULTIPLE, "provided range")  # :13
     check(MPI.Query_thread() == provided, "Query_thread")   # :14
     check(MPI.Is_thread_main(), "Is_thread_main")           # :15
@@ -95,40 +161,28 @@ def main():
             check(bool((got2 == 5.0).all()), "message sent beside a fence")
             MPI.Win_fence(0, win)
         MPI.free(win)
-        # collectives on distinct communicators from distinct threads at once
-        # (each communicator's calls stay ordered, as MPI requires): every
-        # thread runs a loop of Allreduce! (LL, one-shot and zero-copy sizes)
-        # and Bcast! on its own Comm_dup of COMM_WORLD
-        comms = [MPI.Comm_dup(comm) for _ in range(3)]
-        results = [None] * len(comms)
+        # Puts to one target from 8 threads inside one fence epoch, 64 each:
+        # far more than the 16-envelope ring per (origin, target), so threads
+        # wait for slots while others post (rma.cpp post claims its sequence
+        # number before it can yield the lock)
+        nput = 8 * 64
+        win_buf2 = torch.zeros(nput, dtype=torch.float64, device="cuda")
+        win2 = MPI.Win_create(win_buf2, comm)
+        vals = torch.arange(nput, dtype=torch.float64, device="cuda") + 10000.0 * rank
+        MPI.Win_fence(0, win2)
 
-        def loop(i):
-            cm = comms[i]
-            ok = True
-            # each thread on its own stream (the mirror runs a communicator's
-            # collectives on the caller's current stream; two communicators'
-            # kernels queued on ONE stream in different orders on different
-            # ranks would wait for each other — the rule NCCL / RCCL state
-            # for concurrent communicators too)
-            torch.cuda.set_stream(torch.cuda.Stream())
-            for it, cnt in enumerate((7, 1000, 60000, (32 << 20) // 4, 5)):
-                x = torch.full((cnt,), float(rank + 1 + i), device="cuda")
-                y = MPI.Allreduce(x, MPI.SUM, cm)
-                ok &= bool((y == float(sum(q + 1 + i for q in range(size)))).all())
-                b = torch.full((cnt,), float(it) if rank == 0 else -1.0, device="cuda")
-                MPI.Bcast_(b, 0, cm)
-                ok &= bool((b == float(it)).all())
-            torch.cuda.synchronize()
-            results[i] = ok
+        def putter(k):
+            for j in range(64):
+                i = k * 64 + j
+                MPI.Put(vals[i:i + 1], 1, dst, i, win2)
 
-        ths = [threading.Thread(target=loop, args=(i,)) for i in range(len(comms))]
-        for t in ths:
-            t.start()
-        for t in ths:
-            t.join(120)
-        check(all(results) and not any(t.is_alive() for t in ths), f"concurrent collectives on {len(comms)} comms: {results}")
-        for cm in comms:
-            MPI.free(cm)
+        with ThreadPoolExecutor(max_workers=8) as ex:
+            list(ex.map(putter, range(8)))
+        MPI.Win_fence(0, win2)
+        want2 = torch.arange(nput, dtype=torch.float64, device="cuda") + 10000.0 * src
+        check(torch.equal(win_buf2, want2), "512 Puts to one target from 8 threads in one epoch")
+        MPI.free(win2)
+        concurrent_comms(comm, size, rank, stuck_mode=False)
     MPI.Barrier(comm)
     MPI.Finalize()
     print(json.dumps({"rank": MPI.Comm_rank(comm), "provided": provided, "checks": NCHECK[0],

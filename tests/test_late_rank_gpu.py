@@ -32,8 +32,11 @@ def _results(outs):
                                              ("xdev", 2, "late_small"), ("xdev", 3, "late"),
                                              ("xdev", 2, "late_vx"), ("xdev", 2, "late_so"),
                                              ("xdev", 2, "late_so_small"), ("gate", 3, "late_so_small"),
-                                             ("xdev", 2, "late_p2p")])
+                                             ("xdev", 2, "late_p2p"), ("xdev", 2, "late_stream")])
 def test_late_rank_is_waited_for(cfg, n, scenario):
+    """(~130 s) A rank 2.5 x MPIGX_TIMEOUT_MS late — on its host, or on its
+    GPU behind earlier stream work (late_stream) — is waited
+    for: exact results, no error."""
     rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=(scenario,))
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-2000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     assert all(rc == 0 for rc in rcs), msg
