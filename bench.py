@@ -306,7 +306,24 @@ def bench_local(args):
         e1.record(stream)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / reps * 1e3
-        sweep[f"{mib}MiB"] = {"GBps": round((args.nbuf + 1) * k * 4 / (us / 1e6) / 1e9, 1), "us": round(us, 2)}
+        # the same launches replayed from one captured HIP graph: the host's
+        # per-launch cost out of the loop (below ~4 MiB the eager loop above
+        # is bound by the host issuing launches, not by the kernel)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(reps):
+                MPI.reduce_local_multi(xs, o, MPI.SUM)
+        graph.replay()
+        torch.cuda.synchronize()
+        e0.record(stream)
+        graph.replay()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        usg = e0.elapsed_time(e1) / reps * 1e3
+        del graph
+        sweep[f"{mib}MiB"] = {"GBps": round((args.nbuf + 1) * k * 4 / (us / 1e6) / 1e9, 1), "us": round(us, 2),
+                              "GBps_graph": round((args.nbuf + 1) * k * 4 / (usg / 1e6) / 1e9, 1),
+                              "us_graph": round(usg, 2)}
     sweep[f"{args.mib}MiB"] = {"GBps": round(algo / (kern_ms / 1e3) / 1e9, 1), "us": round(kern_ms * 1e3, 2)}
     cpu_ar = None if args.no_cpu_baseline else cpu_reference_allreduce()
 

@@ -677,7 +677,16 @@ int finish(mpigx_comm* c) {
             for (int q = 0; q < c->n && late < 0; ++q)
               if (q != c->rank && c->shm->ranks[q].kseq_run.load(std::memory_order_acquire) < seen) late = q;
             if (late < 0) {
-              why = "every rank's GPU is in this launch and none has moved (protocol stall)";
+              // partial residency: every rank's block 0 started but not all
+              // blocks are resident — the same cause as a stuck peer when
+              // other communicators' collectives are in flight somewhere
+              bool others = busy_comms() >= 2;
+              for (int q = 0; q < c->n && !others; ++q)
+                others = c->shm->ranks[q].proc_busy.load(std::memory_order_relaxed) >= 2;
+              why = others ? "every rank's GPU is in this launch and none has moved while other communicators' "
+                             "collectives run (their grids do not fit on the GPU together: set "
+                             "MPIGX_CONCURRENT_COMMS to the number of communicators in flight at once)"
+                           : "every rank's GPU is in this launch and none has moved (protocol stall)";
             } else if (!noted) {
               noted = true;
               fprintf(stderr, "mpigx: rank %d has waited %.0f s for rank %d to reach the collective\n", c->rank, el,

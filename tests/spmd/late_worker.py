@@ -107,7 +107,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.time()
         if r == n - 1:
-            torch.cuda._sleep(int(2.5 * timeout_s / per_cycle_s))
+            torch.cuda._sleep(int(3.0 * timeout_s / per_cycle_s))
         MPI.Allreduce_(send, recv, MPI.SUM, comm)
         out["late_call_s"] = round(time.time() - t0, 3)
         if not bool((recv == want).all()):

@@ -15,6 +15,7 @@ import json
 import os
 import sys
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -53,17 +54,12 @@ def exchange(comm, n_msgs, nthreads, tag0):
     return torch.equal(recv_arr, want)
 
 
-def concurrent_comms(comm, size, rank, stuck_mode):
+def concurrent_comms(comm, size, rank):
     """Collectives on distinct communicators from distinct threads at once
     (each communicator's calls stay ordered, as MPI requires): every thread
     runs a loop of Allreduce! (LL, one-shot and zero-copy sizes) and Bcast!
-    on its own Comm_dup of COMM_WORLD.  With MPIGX_CONCURRENT_COMMS covering
-    the three communicators every result must be exact.  stuck_mode (the
-    launcher leaves the knob at 1): the three grids need not fit on the GPU
-    together, and a launch stuck behind the other communicators' kernels
-    must end its call with MPI_ERR_OTHER (mpigx.cpp stuck_peer) instead of
-    waiting forever; every thread has to come back either way, and every
-    result that is returned must be exact."""
+    on its own Comm_dup of COMM_WORLD.  MPIGX_CONCURRENT_COMMS covers the
+    three communicators: every result must be exact."""
     comms = [MPI.Comm_dup(comm) for _ in range(3)]
     results = [None] * len(comms)
 
@@ -76,46 +72,91 @@ def concurrent_comms(comm, size, rank, stuck_mode):
         # ranks would wait for each other — the rule NCCL / RCCL state
         # for concurrent communicators too)
         torch.cuda.set_stream(torch.cuda.Stream())
-        try:
-            for rep in range(3 if stuck_mode else 1):
-                for it, cnt in enumerate((7, 1000, 60000, (32 << 20) // 4, 5)):
-                    x = torch.full((cnt,), float(rank + 1 + i), device="cuda")
-                    y = MPI.Allreduce(x, MPI.SUM, cm)
-                    ok &= bool((y == float(sum(q + 1 + i for q in range(size)))).all())
-                    b = torch.full((cnt,), float(it) if rank == 0 else -1.0, device="cuda")
-                    MPI.Bcast_(b, 0, cm)
-                    ok &= bool((b == float(it)).all())
-            torch.cuda.synchronize()
-            results[i] = ok
-        except MPI.MPIError as e:
-            results[i] = f"MPIError {e.code}"
+        for it, cnt in enumerate((7, 1000, 60000, (32 << 20) // 4, 5)):
+            x = torch.full((cnt,), float(rank + 1 + i), device="cuda")
+            y = MPI.Allreduce(x, MPI.SUM, cm)
+            ok &= bool((y == float(sum(q + 1 + i for q in range(size)))).all())
+            b = torch.full((cnt,), float(it) if rank == 0 else -1.0, device="cuda")
+            MPI.Bcast_(b, 0, cm)
+            ok &= bool((b == float(it)).all())
+        torch.cuda.synchronize()
+        results[i] = ok
 
     ths = [threading.Thread(target=loop, args=(i,)) for i in range(len(comms))]
     for t in ths:
         t.start()
     for t in ths:
+        t.join(120)
+    check(all(results) and not any(t.is_alive() for t in ths), f"concurrent collectives on {len(comms)} comms: {results}")
+    for cm in comms:
+        MPI.free(cm)
+
+
+def stuck_case(comm, size, rank):
+    """More communicators in flight than the GPU holds resident together
+    (VERDICT r05 item 2), made deterministic: three communicators, each
+    Allreduce! of 64 MiB (zero-copy) on its own thread and stream, grids at
+    their residency cap (MPIGX_MAX_BLOCKS raised by the launcher, so each
+    grid takes its share of the device: with MPIGX_CONCURRENT_COMMS = 1 the
+    three of one rank fill it).  Rank 0 launches first; the other ranks
+    0.5 s later find no room, and their launches never start while rank 0's
+    grids wait for them.  With MPIGX_CONCURRENT_COMMS = 1 every call must
+    come back with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS (mpigx.cpp
+    stuck_peer / the stall rule; stderr names the knob); with the knob at
+    the number of communicators every result must be exact."""
+    ncomm = 3
+    comms = [MPI.Comm_dup(comm) for _ in range(ncomm)]
+    cnt = (64 << 20) // 4
+    xs = [torch.full((cnt,), float(rank + 1 + i), device="cuda") for i in range(ncomm)]
+    ys = [torch.empty_like(x) for x in xs]
+    want = [float(sum(q + 1 + i for q in range(size))) for i in range(ncomm)]
+    streams = [torch.cuda.Stream() for _ in range(ncomm)]
+    # one communicator at a time first: buffer registration and the
+    # algorithm tuner's sampling calls, so the concurrent calls below launch
+    # straight away (no host exchange that would line the ranks up)
+    for i in range(ncomm):
+        with torch.cuda.stream(streams[i]):
+            for _ in range(6):
+                MPI.Allreduce_(xs[i], ys[i], MPI.SUM, comms[i])
+            check(bool((ys[i] == want[i]).all()), f"warm-up comm {i}")
+    torch.cuda.synchronize()
+    MPI.Barrier(comm)
+    results, secs = [None] * ncomm, [None] * ncomm
+
+    def run(i):
+        torch.cuda.set_stream(streams[i])
+        if rank != 0:
+            time.sleep(0.5)
+        t0 = time.time()
+        try:
+            ys[i].fill_(-1)
+            MPI.Allreduce_(xs[i], ys[i], MPI.SUM, comms[i])
+            results[i] = bool((ys[i] == want[i]).all())
+        except MPI.MPIError as e:
+            results[i] = f"MPIError {e.code}"
+        secs[i] = round(time.time() - t0, 3)
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(ncomm)]
+    for t in ths:
+        t.start()
+    for t in ths:
         t.join(180)
     alive = any(t.is_alive() for t in ths)
-    if not stuck_mode:
-        check(all(r is True for r in results) and not alive, f"concurrent collectives on {len(comms)} comms: {results}")
-    else:
-        errs = [r for r in results if isinstance(r, str)]
-        check(not alive, f"every thread came back: {results}")
-        check(all(r is True or r == f"MPIError {MPI.consts.MPI_ERR_OTHER}" for r in results), f"results: {results}")
-        print(json.dumps({"rank": rank, "stuck_results": results, "errors": len(errs)}), flush=True)
+    check(not alive, f"every thread came back: {results}")
+    check(all(r is True or r == f"MPIError {MPI.consts.MPI_ERR_OTHER}" for r in results), f"results: {results}")
+    print(json.dumps({"rank": rank, "stuck_results": results, "call_s": secs,
+                      "errors": sum(isinstance(r, str) for r in results)}), flush=True)
     for cm in comms:
         try:
             MPI.free(cm)
         except MPI.MPIError:
             pass  # a communicator that failed above
-    return results
-
 
 def main():
     provided = MPI.Init_thread(MPI.THREAD_MULTIPLE)       # test_threads.jl:11
     if os.environ.get("THREADS_MODE") == "stuck":
         comm = MPI.COMM_WORLD
-        concurrent_comms(comm, MPI.Comm_size(comm), MPI.Comm_rank(comm), stuck_mode=True)
+        stuck_case(comm, MPI.Comm_size(comm), MPI.Comm_rank(comm))
         MPI.Barrier(comm)
         MPI.Finalize()
         print(json.dumps({"rank": MPI.Comm_rank(comm), "provided": provided, "checks": NCHECK[0],
@@ -182,7 +223,7 @@ def main():
         want2 = torch.arange(nput, dtype=torch.float64, device="cuda") + 10000.0 * src
         check(torch.equal(win_buf2, want2), "512 Puts to one target from 8 threads in one epoch")
         MPI.free(win2)
-        concurrent_comms(comm, size, rank, stuck_mode=False)
+        concurrent_comms(comm, size, rank)
     MPI.Barrier(comm)
     MPI.Finalize()
     print(json.dumps({"rank": MPI.Comm_rank(comm), "provided": provided, "checks": NCHECK[0],

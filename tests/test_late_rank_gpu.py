@@ -43,7 +43,9 @@ def test_late_rank_is_waited_for(cfg, n, scenario):
     res = _results(outs)
     assert len(res) == n and all(not x["fails"] for x in res), res
     early = [x["late_call_s"] for x in res if x["rank"] != n - 1]
-    assert min(early) >= 2.0 * 2.0, res  # they waited past their 2 s timeout
+    # they waited past their 2 s timeout (late_stream: the late rank's GPU
+    # work is sized by a calibrated torch.cuda._sleep, so only "well past")
+    assert min(early) >= (1.5 if scenario == "late_stream" else 2.0) * 2.0, res
 
 
 @pytest.mark.parametrize("cfg,scenario", [("gate", "gone"), ("xdev", "gone"), ("xdev", "gone_so"),

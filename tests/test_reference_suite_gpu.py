@@ -39,21 +39,29 @@ def test_reference_threads_device(n):
     assert len(summ) == n and all(s["nfail"] == 0 and s["provided"] == 3 for s in summ), summ
 
 
-def test_concurrent_comms_stuck_is_an_error():
-    """VERDICT r05 item 2 (~30 s): the threads worker's three-communicator
-    case at n = 3 on one GPU with MPIGX_CONCURRENT_COMMS left at 1, where the
-    three grids need not fit on the GPU together (round 5: stalled without
-    end).  A launch stuck behind the other communicators' kernels now ends
-    its call with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS (mpigx.cpp
-    stuck_peer), naming MPIGX_CONCURRENT_COMMS; every thread of every rank
-    comes back, and every result that is returned is exact."""
-    env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "5000", "MPIGX_CONCURRENT_COMMS": "1",
+@pytest.mark.parametrize("k", [1, 3])
+def test_concurrent_comms_beyond_residency(k):
+    """(~40 s) VERDICT r05 item 2: three communicators' 64 MiB Allreduce! at
+    once from three threads per rank, n = 3 on one GPU, no host gate (the
+    one-rank-per-GPU protocol), grids at their residency caps, rank 0 first
+    (tests/spmd/threads_worker.py stuck_case).  k = 1: the grids cannot all
+    be resident, which waited forever in round 5; now every call of every
+    rank ends with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS and stderr
+    names MPIGX_CONCURRENT_COMMS.  k = 3 (the knob at the number of
+    communicators): exact."""
+    env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "3000", "MPIGX_CONCURRENT_COMMS": str(k),
+           "MPIGX_MAX_BLOCKS": "4096", "MPIGX_SHARED_GATE": "0", "MPIGX_PEER_MEM": "xdev",
            "THREADS_MODE": "stuck"}
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "threads_worker.py"), 3, timeout=240, extra_env=env)
+    msg = "\n".join(o[-3000:] for o in outs)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
     stuck = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"stuck_results"' in l]
-    assert all(rc == 0 for rc in rcs), "\n".join(o[-2000:] for o in outs)
+    assert all(rc == 0 for rc in rcs), msg
     assert len(summ) == 3 and all(s["nfail"] == 0 for s in summ), summ
-    print("stuck-mode results:", stuck)
-    if any(s["errors"] for s in stuck):  # a stall happened: the engine said why
-        assert any("MPIGX_CONCURRENT_COMMS" in o for o in outs), "\n".join(o[-2000:] for o in outs)
+    assert len(stuck) == 3, msg
+    if k == 1:
+        assert all(s["errors"] >= 1 for s in stuck), stuck
+        assert all(t < 3.0 * 3 + 10 for s in stuck for t in s["call_s"]), stuck
+        assert "MPIGX_CONCURRENT_COMMS" in msg, msg
+    else:
+        assert all(r is True for s in stuck for r in s["stuck_results"]), stuck

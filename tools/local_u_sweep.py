@@ -2,7 +2,10 @@
 16-B vectors per thread (MPIGX_LOCAL_U forces one; unset = the product rule,
 common.hpp local_u) — the measurement behind the size rule (VERDICT r05
 item 4).  HIP events on the launch stream over 50 back-to-back launches.
-Prints one JSON line.  Run on the GPU box from the repo root."""
+Each size also replays the launches from one captured HIP graph (us_graph),
+which takes the host's per-launch cost out: below ~4 MiB the eager loop is
+bound by the host issuing launches, not by the kernel.  Prints one JSON
+line.  Run on the GPU box from the repo root."""
 import json
 import os
 import sys
@@ -45,7 +48,23 @@ def main():
             b.record(s)
             torch.cuda.synchronize()
             us = a.elapsed_time(b) / reps * 1e3
-            row[f"{mib}MiB"] = {"us": round(us, 2), "GBps": round((nbuf + 1) * k * 4 / (us / 1e6) / 1e9, 1)}
+            # the same launches captured in one HIP graph and replayed: no
+            # host launch cost between kernels (device-bound per-launch time)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for _ in range(reps):
+                    MPI.reduce_local_multi(xs, o, MPI.SUM)
+            graph.replay()
+            torch.cuda.synchronize()
+            a.record(s)
+            graph.replay()
+            b.record(s)
+            torch.cuda.synchronize()
+            usg = a.elapsed_time(b) / reps * 1e3
+            row[f"{mib}MiB"] = {"us": round(us, 2), "GBps": round((nbuf + 1) * k * 4 / (us / 1e6) / 1e9, 1),
+                                "us_graph": round(usg, 2),
+                                "GBps_graph": round((nbuf + 1) * k * 4 / (usg / 1e6) / 1e9, 1)}
+            del graph
         # correctness of the last (largest) size against torch's own sum order is
         # not the point here; the GPU suite checks bits.  Keep the output used.
         res[f"U={u}"] = row
