@@ -317,6 +317,10 @@ int shared_gate(mpigx_comm* c) {
 // ended.  What separates the two: the stuck peer's HOST enqueued the launch
 // long ago (kseq_enq), its GPU has not started it (kseq_run), and its
 // process has another communicator's collective in flight (proc_busy >= 2).
+// The same holds when two communicators' streams share one hardware queue
+// (HIP maps streams onto GPU_MAX_HW_QUEUES queues, 4 by default): a launch
+// queued behind another communicator's spinning kernel cannot start until
+// that kernel ends, and the queue order differs from rank to rank (r06b).
 // busy_comms() is that count for this process: blocking calls inside
 // finish()'s wait, plus stream-ordered communicators whose stream the watcher
 // last found busy.
@@ -354,7 +358,8 @@ int stuck_peer(mpigx_comm* c, unsigned long long L, double t, double tmo) {
 void note_stuck(mpigx_comm* c, int who, double t) {
   fprintf(stderr, "[mpigx] rank %d: rank %d enqueued this launch %.0f s ago but its GPU never started it while "
           "other communicators' collectives run in its process: more communicators are in flight at once than "
-          "the GPU holds resident together (set MPIGX_CONCURRENT_COMMS to their number)\n", c->rank, who,
+          "the GPU holds resident together (set MPIGX_CONCURRENT_COMMS to their number), or their streams share "
+          "a hardware queue (GPU_MAX_HW_QUEUES at least the number of streams in use)\n", c->rank, who,
           t - c->stuck_since[who]);
 }
 

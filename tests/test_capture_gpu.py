@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("n", [2])
 def test_capture_is_refused(n):
+    """(~3 s) A call on a stream under HIP-graph capture is refused with MPI_ERR_OTHER before anything is enqueued; the capture and the communicator stay usable."""
     env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "30000"}
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "capture_worker.py"), n, timeout=300, extra_env=env)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]

@@ -21,6 +21,7 @@ ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS"
 
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_headline_sizes(n):
+    """(~15 s) The 256 MiB default Allreduce path (whole buffer) and every algorithm at 16 MiB / 1 MiB on the production grid, bit-exact against the oracle."""
     env = dict(ENV, MPIGX_HEADLINE_EXTRA="1")
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "headline_worker.py"), n, timeout=900, extra_env=env)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))

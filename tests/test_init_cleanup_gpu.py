@@ -11,6 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_init_timeout_leaks_nothing():
+    """(~1 s) A communicator init that times out releases every resource it took (device memory, pinned page, shm name)."""
     import mpigx
     from mpigx._lib import UniqueId
     L = mpigx.lib()

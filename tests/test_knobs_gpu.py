@@ -26,30 +26,36 @@ def _run(n, scenario, **env):
 
 @pytest.mark.parametrize("scenario", ["mismatch_init", "bad_name"])
 def test_knob_mismatch_fails_at_init(scenario):
+    """(~7 s) Path-selecting knobs that differ between ranks fail comm init on every rank."""
     extra = {"MPIGX_ALGO": "warp"} if scenario == "bad_name" else {}
     res = _run(2, scenario, **extra)
     assert all(x["code"] == 12 for x in res), res
 
 
 def test_set_knob_is_collective():
+    """(~4 s) mpigx_comm_set_knob changes a path-selecting knob collectively; results stay exact across the change."""
     _run(2, "set_knob")
 
 
 @pytest.mark.parametrize("n", [2, 4])
 def test_device_share_and_grid_cap(n):
+    """(~8 s) Ranks sharing a device are counted and the spinning kernels' grids capped for residency."""
     res = _run(n, "share")
     print(res[0])
 
 
 def test_device_share_limit():
+    """(~3 s) More ranks per device than MPIGX_MAX_RANKS_PER_DEVICE fail init with MPI_ERR_OTHER."""
     res = _run(2, "share_limit", MPIGX_MAX_RANKS_PER_DEVICE="1")
     assert all(x["code"] == 15 for x in res), res
 
 
 def test_zero_copy_import_failure_agreed():
+    """(~4 s) A failed peer import is agreed by every rank, which all take the staged path: exact results."""
     _run(2, "import_fail")
 
 
 @pytest.mark.parametrize("base", [(1 << 31) - 12, (1 << 31) - 36])
 def test_ll_flag_generation_wrap(base):
+    """(~7 s) LL flags across the 2^31 epoch generation boundary (area cleared, no stale flag accepted)."""
     _run(2, "ll_wrap", MPIGX_EPOCH_BASE=str(base))

@@ -28,13 +28,22 @@ def _results(outs):
     return [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"scenario"' in l]
 
 
-@pytest.mark.parametrize("cfg,n,scenario", [("gate", 2, "late"), ("gate", 4, "late"), ("xdev", 2, "late"),
-                                             ("xdev", 2, "late_small"), ("xdev", 3, "late"),
-                                             ("xdev", 2, "late_vx"), ("xdev", 2, "late_so"),
-                                             ("xdev", 2, "late_so_small"), ("gate", 3, "late_so_small"),
-                                             ("xdev", 2, "late_p2p"), ("xdev", 2, "late_stream")])
+# every case waits 2.5 x the 2 s timeout for the late rank: four cover the
+# protocols (host gate; one-rank-per-GPU blocking, stream-ordered, and a
+# rank late on its own stream), the rest are `slow`
+SLOW = pytest.mark.slow
+@pytest.mark.parametrize("cfg,n,scenario", [("gate", 2, "late"), pytest.param("gate", 4, "late", marks=SLOW),
+                                             ("xdev", 2, "late"),
+                                             pytest.param("xdev", 2, "late_small", marks=SLOW),
+                                             pytest.param("xdev", 3, "late", marks=SLOW),
+                                             pytest.param("xdev", 2, "late_vx", marks=SLOW),
+                                             pytest.param("xdev", 2, "late_so", marks=SLOW),
+                                             ("xdev", 2, "late_so_small"),
+                                             pytest.param("gate", 3, "late_so_small", marks=SLOW),
+                                             pytest.param("xdev", 2, "late_p2p", marks=SLOW),
+                                             ("xdev", 2, "late_stream")])
 def test_late_rank_is_waited_for(cfg, n, scenario):
-    """(~130 s) A rank 2.5 x MPIGX_TIMEOUT_MS late — on its host, or on its
+    """(~35 s) A rank 2.5 x MPIGX_TIMEOUT_MS late — on its host, or on its
     GPU behind earlier stream work (late_stream) — is waited
     for: exact results, no error."""
     rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=(scenario,))
@@ -48,9 +57,10 @@ def test_late_rank_is_waited_for(cfg, n, scenario):
     assert min(early) >= (1.5 if scenario == "late_stream" else 2.0) * 2.0, res
 
 
-@pytest.mark.parametrize("cfg,scenario", [("gate", "gone"), ("xdev", "gone"), ("xdev", "gone_so"),
-                                          ("xdev", "gone_p2p")])
+@pytest.mark.parametrize("cfg,scenario", [("gate", "gone"), pytest.param("xdev", "gone", marks=SLOW),
+                                          ("xdev", "gone_so"), pytest.param("xdev", "gone_p2p", marks=SLOW)])
 def test_vanished_rank_fails_the_call(cfg, scenario):
+    """(~8 s) A rank that exits without finalizing fails its peers' next call within seconds."""
     n = 3
     rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=(scenario,))
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-2000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
@@ -62,7 +72,7 @@ def test_vanished_rank_fails_the_call(cfg, scenario):
 
 @pytest.mark.parametrize("cfg", ["gate", "xdev"])
 def test_broken_peer_fails_the_call(cfg):
-    """a rank whose communicator already failed never reaches the
+    """(~7 s) ADVICE r04: a rank whose communicator already failed never reaches the
     gate or launches; its peers learn it from the shm block (ShmRank.broken)
     and fail within seconds instead of waiting for it."""
     n = 3

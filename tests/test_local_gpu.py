@@ -62,6 +62,7 @@ def expected(ins, dtname, opname, order):
 
 @pytest.mark.parametrize("dtname,opname", valid_pairs(REPRESENTATIVE))
 def test_all_ops_types(L, dtname, opname):
+    """(~1 s) Every valid (op, type) pair of the local fold, bit-exact against the MPICH-pinned oracle."""
     for n, count, seed in ((8, 1037, 1), (3, 517, 2), (5, 4099, 3), (2, 64, 4)):
         ins = make(dtname, opname, n, count, seed, edge=True)
         for order in (0, 1):
@@ -71,6 +72,7 @@ def test_all_ops_types(L, dtname, opname):
 
 @pytest.mark.parametrize("n", [1, 2, 4, 6, 7, 8, 9, 12, 13, 15, 16])
 def test_rank_counts(L, n):
+    """(~1 s) The local fold at 1..16 inputs against the oracle's association."""
     for dtname, opname in (("FLOAT", "SUM"), ("FLOAT", "MAX"), ("INT64_T", "BXOR"), ("DOUBLE", "MIN")):
         for count in (7, 300, 20011):
             ins = make(dtname, opname, n, count, 10 + n, edge=True)
@@ -80,7 +82,7 @@ def test_rank_counts(L, n):
 
 
 def test_full_shape_multi_vector(L):
-    """The 8-buffer shape (SH_FULL, U vectors per thread): sizes with whole and
+    """(~1 s) The 8-buffer shape (SH_FULL, U vectors per thread): sizes with whole and
     partial U-blocks, Rabenseifner block boundaries inside a vector (count/8
     not a multiple of the vector width) and ragged tails, every op family."""
     for dtname, opname in (("FLOAT", "SUM"), ("FLOAT", "MAX"), ("BFLOAT16", "SUM"), ("BFLOAT16", "MAX"),
@@ -92,7 +94,7 @@ def test_full_shape_multi_vector(L):
 
 
 def test_bf16_random_bit_patterns(L):
-    """bf16 definition (fp32 compute, RNE to bf16 after every op, NaN quiet) on
+    """(~1 s) bf16 definition (fp32 compute, RNE to bf16 after every op, NaN quiet) on
     uniformly random 16-bit patterns — NaN payloads, infinities, denormals,
     rounding ties — through the packed pair ops (v_pk_add/mul_f32 +
     v_cvt_pk_bf16_f32) against the oracle's software rounding."""
@@ -105,6 +107,7 @@ def test_bf16_random_bit_patterns(L):
 
 
 def test_unaligned_and_empty(L):
+    """(~1 s) Unaligned inputs / output and empty counts through the local fold."""
     ins = make("FLOAT", "SUM", 8, 1001, 7)
     for pad in (1, 4, 8, 12):
         got = run_multi(L, ins, "FLOAT", "SUM", 0, pad=pad)
@@ -115,6 +118,7 @@ def test_unaligned_and_empty(L):
 
 
 def test_invalid_pairs_rejected(L):
+    """(~1 s) (op, type) pairs MPICH rejects return MPI_ERR_OP before any launch."""
     t = torch.zeros(16, dtype=torch.uint8, device="cuda")
     ptrs = (ctypes.c_void_p * 2)(t.data_ptr(), t.data_ptr())
     for dtname, opname, code in (("FLOAT", "BAND", 9), ("C_FLOAT_COMPLEX", "MAX", 9), ("BYTE", "SUM", 9),
@@ -127,7 +131,7 @@ def test_invalid_pairs_rejected(L):
 
 
 def test_reduce_local_matches_mpich_fixtures(L):
-    """MPI_Reduce_local golden vectors (MPICH 3.3.2) through mpigx_reduce_local."""
+    """(~1 s) MPI_Reduce_local golden vectors (MPICH 3.3.2) through mpigx_reduce_local."""
     from golden_io import load, typed
     cases, arr = load()
     bad = []

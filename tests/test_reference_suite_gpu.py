@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("n,cfg", [(2, "same"), (4, "same"), (3, "xdev"), (8, "xdev")])
 def test_reference_suite_device(n, cfg):
-    """cfg xdev: the one-rank-per-GPU signalling (MPIGX_PEER_MEM=xdev, no host
+    """(~15 s) cfg xdev: the one-rank-per-GPU signalling (MPIGX_PEER_MEM=xdev, no host
     gate; tests/test_xdev_gpu.py), at n = 8 the driver node's rank count."""
     env = {"MPIGX_TEST_ARRAYTYPE": "ROCArray", "MPIGX_DEVICE": "0", "MPIGX_MAX_BLOCKS": "16",
            "MPIGX_TIMEOUT_MS": "30000", "MPIGX_STAGING_BYTES": str(16 << 20)}
@@ -27,12 +27,18 @@ def test_reference_suite_device(n, cfg):
 
 @pytest.mark.parametrize("n", [2, 3])
 def test_reference_threads_device(n):
-    """test/test_threads.jl in device mode (tests/spmd/threads_worker.py):
+    """(~10 s) test/test_threads.jl in device mode (tests/spmd/threads_worker.py):
     Init_thread(THREAD_MULTIPLE), threaded Irecv! / Isend of one-element
     device views, Waitall on the main thread."""
     # the worker runs collectives of three communicators at once: their
     # spinning kernels must fit on the GPU together (MPIGX_CONCURRENT_COMMS)
-    env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "30000", "MPIGX_CONCURRENT_COMMS": "4"}
+    # ... and every stream of a rank its own hardware queue: HIP maps streams
+    # onto GPU_MAX_HW_QUEUES queues (4 by default), and two communicators'
+    # kernels sharing one queue wait for each other in queue order —
+    # differently on each rank (r06b: a deadlock the stuck-peer rule turned
+    # into MPI_ERR_OTHER after 30 s; INTEGRATION.md "Threads")
+    env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "30000", "MPIGX_CONCURRENT_COMMS": "4",
+           "GPU_MAX_HW_QUEUES": "16"}
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "threads_worker.py"), n, timeout=300, extra_env=env)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
     assert all(rc == 0 for rc in rcs), "\n".join(o[-2000:] for o in outs)
@@ -41,7 +47,7 @@ def test_reference_threads_device(n):
 
 @pytest.mark.parametrize("k", [1, 3])
 def test_concurrent_comms_beyond_residency(k):
-    """(~40 s) VERDICT r05 item 2: three communicators' 64 MiB Allreduce! at
+    """(~12 s) VERDICT r05 item 2: three communicators' 64 MiB Allreduce! at
     once from three threads per rank, n = 3 on one GPU, no host gate (the
     one-rank-per-GPU protocol), grids at their residency caps, rank 0 first
     (tests/spmd/threads_worker.py stuck_case).  k = 1: the grids cannot all
@@ -51,7 +57,7 @@ def test_concurrent_comms_beyond_residency(k):
     communicators): exact."""
     env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "3000", "MPIGX_CONCURRENT_COMMS": str(k),
            "MPIGX_MAX_BLOCKS": "4096", "MPIGX_SHARED_GATE": "0", "MPIGX_PEER_MEM": "xdev",
-           "THREADS_MODE": "stuck"}
+           "THREADS_MODE": "stuck", "GPU_MAX_HW_QUEUES": "16"}
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "threads_worker.py"), 3, timeout=240, extra_env=env)
     msg = "\n".join(o[-3000:] for o in outs)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
