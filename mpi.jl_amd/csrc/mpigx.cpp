@@ -337,9 +337,11 @@ int busy_comms() {
 }
 // The first peer that has been stuck in launch L (enqueued, never started,
 // other communicators busy in its process) for longer than tmo seconds, or
-// -1.  c->stuck_since[q] remembers when q was first seen so; any other state
-// resets it.  Called every 0.25 s.
-int stuck_peer(mpigx_comm* c, unsigned long long L, double t, double tmo) {
+// -1.  since[q] remembers when q was first seen so; any other state resets
+// it.  Called every 0.25 s, by finish() with c->stuck_since and by the
+// watcher thread with c->wstuck_since (a communicator can have both: a
+// blocking call after stream-ordered launches).
+int stuck_peer(mpigx_comm* c, unsigned long long L, double t, double tmo, double* since) {
   int who = -1;
   for (int q = 0; q < c->n; ++q) {
     if (q == c->rank) continue;
@@ -347,20 +349,20 @@ int stuck_peer(mpigx_comm* c, unsigned long long L, double t, double tmo) {
     const bool s = sr.kseq_enq.load(std::memory_order_relaxed) >= L &&
                    sr.kseq_run.load(std::memory_order_acquire) < L && sr.proc_busy.load(std::memory_order_relaxed) >= 2;
     if (!s) {
-      c->stuck_since[q] = 0;
+      since[q] = 0;
       continue;
     }
-    if (c->stuck_since[q] == 0) c->stuck_since[q] = t;
-    if (who < 0 && t - c->stuck_since[q] > tmo) who = q;
+    if (since[q] == 0) since[q] = t;
+    if (who < 0 && t - since[q] > tmo) who = q;
   }
   return who;
 }
-void note_stuck(mpigx_comm* c, int who, double t) {
+void note_stuck(mpigx_comm* c, int who, double t, const double* since) {
   fprintf(stderr, "[mpigx] rank %d: rank %d enqueued this launch %.0f s ago but its GPU never started it while "
           "other communicators' collectives run in its process: more communicators are in flight at once than "
           "the GPU holds resident together (set MPIGX_CONCURRENT_COMMS to their number), or their streams share "
           "a hardware queue (GPU_MAX_HW_QUEUES at least the number of streams in use)\n", c->rank, who,
-          t - c->stuck_since[who]);
+          t - since[who]);
 }
 
 // Stream-ordered (RCCL-style) launches wait for a late peer too (round 5):
@@ -415,9 +417,9 @@ void watch_one(mpigx_comm* c, bool check) {
   // still has work: launch st has not completed here)
   const double tmo = c->timeout_ticks / 1e8;
   if (!why && st > 0 && c->watch_busy && t - c->watch_moved > tmo) {
-    who = stuck_peer(c, st, t, tmo);
+    who = stuck_peer(c, st, t, tmo, c->wstuck_since);
     if (who >= 0) {
-      note_stuck(c, who, t);
+      note_stuck(c, who, t, c->wstuck_since);
       why = "stuck behind other communicators' kernels";
     }
   }
@@ -670,9 +672,9 @@ int finish(mpigx_comm* c) {
           // stuck / stall rules below judge the peers against THAT launch
           const bool mine_running = seen > c->kseq_done;
           if (!why && mine_running) {
-            const int stuck = stuck_peer(c, seen, t, tmo);
+            const int stuck = stuck_peer(c, seen, t, tmo, c->stuck_since);
             if (stuck >= 0) {
-              note_stuck(c, stuck, t);
+              note_stuck(c, stuck, t, c->stuck_since);
               who = stuck;
               why = "stuck behind other communicators' kernels";
             }

@@ -194,7 +194,8 @@ struct mpigx_comm {
   unsigned long long kseq_done = 0;  // launches known complete (kseq when the last finish() returned)
   // stuck-peer tracking (mpigx.cpp stuck_peer): since when rank q has been
   // seen enqueued-but-not-started in the awaited launch (0: not seen so)
-  double stuck_since[mpigx::kMaxRanks] = {};
+  double stuck_since[mpigx::kMaxRanks] = {};   // finish()'s (the calling thread)
+  double wstuck_since[mpigx::kMaxRanks] = {};  // the watcher thread's (stream-ordered launches)
   // the watcher's view of a stream-ordered communicator: the launch its GPU
   // last reported started, since when, and whether its stream had work
   unsigned long long watch_seen = 0;
