@@ -113,6 +113,32 @@ def cpu_reference_allreduce(ranks=8, mib=256, iters=3):
             "kind": "reference", "impl": "MPICH 3.3.2 MPI_Allreduce f32 SUM, host buffers", **host_cpu()}
 
 
+def cpu_reference_sweep(ranks=8, maxmib=256):
+    """BASELINE.md's CPU plan in the same run: MPICH 3.3.2 under `mpiexec -n
+    ranks` on the host cores — Allreduce f32 SUM at the GPU sweep's sizes,
+    Bcast / Allgather / Alltoall at config 4's, Scan / Exscan / Reduce
+    Int32/Int64 BAND/BOR/MAX at 1 Ki / 1 Mi / 16 Mi elements (config 5's
+    64 Mi bounded: MPICH's Scan moves ~0.1 GB/s per rank), called like
+    collective.jl's ccall sites (oracle/mpich_bench.c `sweep`)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "mpich_bench")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    if not (os.path.exists(exe) and os.path.exists(mpiexec)):
+        return {"error": "MPICH harness not built (oracle/Makefile) or mpiexec missing"}
+    t0 = time.perf_counter()
+    try:
+        out = subprocess.run([mpiexec, "-n", str(ranks), exe, "sweep", str(maxmib)], capture_output=True, text=True,
+                             timeout=400)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    if out.returncode != 0 or not line:
+        return {"error": (out.stderr or out.stdout)[-200:]}
+    j = json.loads(line[-1])
+    j.update({"cores": min(ranks, os.cpu_count() or ranks), "kind": "reference", "impl": "MPICH 3.3.2, host buffers",
+              "wall_s": round(time.perf_counter() - t0, 1), **host_cpu()})
+    return j
+
+
 def cpu_baseline_from_allreduce(cpu_ar):
     """The N > 1 line's cpu_baseline: the reference path itself — MPICH 3.3.2
     MPI_Allreduce(f32 SUM) of the same per-rank size over 8 ranks on this
@@ -807,11 +833,16 @@ def bench_allreduce(args):
                     del xs, pref, mine, out
     guarded("config5", config5_section)
 
-    # the reference path on this box's host cores, same run (rank 0 only)
-    cpu_ar = None
+    # the reference path on this box's host cores, same run (rank 0 only):
+    # the headline Allreduce at 8 ranks (cpu_baseline) and at this run's
+    # rank count, and BASELINE.md's whole CPU plan at 8 ranks
+    cpu_ar = cpu_ar_n = cpu_sweep = None
     if not args.no_cpu_baseline:
         if rank == 0:
             cpu_ar = cpu_reference_allreduce(8, args.mib, 3)
+            if n != 8:
+                cpu_ar_n = cpu_reference_allreduce(n, args.mib, 3)
+            cpu_sweep = cpu_reference_sweep(8, args.mib)
         dist.barrier()
 
     if rank == 0:
@@ -820,7 +851,7 @@ def bench_allreduce(args):
         print(json.dumps(build_coll_line({
             "n": n, "mib": args.mib, "steps": args.steps, "warmup": args.warmup, "t": t, "kern": kern,
             "same_device": same_device, "ar_tune": ar_tune, "traffic": traffic, "traffic_src": traffic_src,
-            "xg": xg, "cpu_ar": cpu_ar, "correct": correct, "tune_classes": tune_classes, "probe": probe,
+            "xg": xg, "cpu_ar": cpu_ar, "cpu_ar_n": cpu_ar_n, "cpu_sweep": cpu_sweep, "correct": correct, "tune_classes": tune_classes, "probe": probe,
             "phases": phases, "section_s": section_s, "sweep": sweep, "rccl": rccl, "cfg4": cfg4,
             "tune_classes4": tune_classes4, "cfg5": cfg5, "cfg5_ok": cfg5_ok[0] and "config5" not in errors,
             "errors": errors})), flush=True)
@@ -877,6 +908,8 @@ def build_coll_line(m):
         # (VERDICT r05 item 1): MPICH MPI_Allreduce, 8 ranks, same size
         "cpu_baseline": cpu_baseline_from_allreduce(m["cpu_ar"]),
         "cpu_reference_allreduce": m["cpu_ar"],
+        "cpu_reference_allreduce_same_ranks": m.get("cpu_ar_n"),
+        "cpu_reference_sweep_8ranks": m.get("cpu_sweep"),
         "correct": m["correct"],
         "ar_tune": m["ar_tune"],
         "tune_classes": m["tune_classes"],

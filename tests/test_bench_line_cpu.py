@@ -93,3 +93,21 @@ def test_coll_line_on_distinct_gpus_and_failed_baseline():
     assert line["cpu_baseline"]["value"] == 1.73
     m["cpu_ar"] = {"error": "timeout"}
     assert bench.build_coll_line(m)["cpu_baseline"] is None
+
+
+def test_cpu_reference_sweep_runs_here():
+    """The N > 1 line's reference sweep (oracle/mpich_bench.c `sweep`, MPICH
+    under mpiexec) at a small size here: every section present, positive
+    rates.  Skipped where MPICH is absent."""
+    import pytest
+    exe = os.path.join(ROOT, "oracle", "_ref", "mpich_bench")
+    if not (os.path.exists(exe) and os.path.exists("/opt/conda/bin/mpiexec")):
+        pytest.skip("MPICH harness not built here")
+    j = bench.cpu_reference_sweep(ranks=2, maxmib=1)
+    assert "error" not in j, j
+    assert j["ranks"] == 2 and j["kind"] == "reference"
+    assert j["allreduce_8KiB"]["busbw_GBps"] > 0 and j["allreduce_1024KiB"]["algbw_GBps"] > 0
+    assert j["movers_64KiB"]["alltoall_busbw_GBps"] > 0 and j["movers_1024KiB"]["bcast_busbw_GBps"] > 0
+    for d in ("int32", "int64"):
+        for o in ("BAND", "BOR", "MAX"):
+            assert j[f"{d}_{o}_1024"]["scan_algbw_GBps"] > 0
