@@ -92,7 +92,7 @@ def concurrent_comms(comm, size, rank):
         MPI.free(cm)
 
 
-def stuck_case(comm, size, rank):
+def stuck_case(comm, size, rank, stream_ordered=False):
     """More communicators in flight than the GPU holds resident together
     (VERDICT r05 item 2), made deterministic: three communicators, each
     Allreduce! of 64 MiB (zero-copy) on its own thread and stream, grids at
@@ -103,10 +103,14 @@ def stuck_case(comm, size, rank):
     grids wait for them.  With MPIGX_CONCURRENT_COMMS = 1 every call must
     come back with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS (mpigx.cpp
     stuck_peer / the stall rule; stderr names the knob); with the knob at
-    the number of communicators every result must be exact."""
+    the number of communicators every result must be exact.
+    stream_ordered: the same with RCCL-style launches (8 MiB, the staged
+    two-shot, which needs no host exchange before its launch): the
+    process-wide watcher (mpigx.cpp watch_one) cancels, and the error comes
+    from mpigx_comm_synchronize."""
     ncomm = 3
     comms = [MPI.Comm_dup(comm) for _ in range(ncomm)]
-    cnt = (64 << 20) // 4
+    cnt = ((8 if stream_ordered else 64) << 20) // 4
     xs = [torch.full((cnt,), float(rank + 1 + i), device="cuda") for i in range(ncomm)]
     ys = [torch.empty_like(x) for x in xs]
     want = [float(sum(q + 1 + i for q in range(size))) for i in range(ncomm)]
@@ -114,11 +118,14 @@ def stuck_case(comm, size, rank):
     # one communicator at a time first: buffer registration and the
     # algorithm tuner's sampling calls, so the concurrent calls below launch
     # straight away (no host exchange that would line the ranks up)
+    L = MPI.lib()
     for i in range(ncomm):
         with torch.cuda.stream(streams[i]):
             for _ in range(6):
                 MPI.Allreduce_(xs[i], ys[i], MPI.SUM, comms[i])
             check(bool((ys[i] == want[i]).all()), f"warm-up comm {i}")
+        if stream_ordered:
+            MPI.api._check(L.mpigx_comm_set_blocking(comms[i].val, 0))
     torch.cuda.synchronize()
     MPI.Barrier(comm)
     results, secs = [None] * ncomm, [None] * ncomm
@@ -131,6 +138,8 @@ def stuck_case(comm, size, rank):
         try:
             ys[i].fill_(-1)
             MPI.Allreduce_(xs[i], ys[i], MPI.SUM, comms[i])
+            if stream_ordered:
+                MPI.api._check(L.mpigx_comm_synchronize(comms[i].val))
             results[i] = bool((ys[i] == want[i]).all())
         except MPI.MPIError as e:
             results[i] = f"MPIError {e.code}"
@@ -154,9 +163,9 @@ def stuck_case(comm, size, rank):
 
 def main():
     provided = MPI.Init_thread(MPI.THREAD_MULTIPLE)       # test_threads.jl:11
-    if os.environ.get("THREADS_MODE") == "stuck":
+    if os.environ.get("THREADS_MODE") in ("stuck", "stuck_so"):
         comm = MPI.COMM_WORLD
-        stuck_case(comm, MPI.Comm_size(comm), MPI.Comm_rank(comm))
+        stuck_case(comm, MPI.Comm_size(comm), MPI.Comm_rank(comm), os.environ["THREADS_MODE"] == "stuck_so")
         MPI.Barrier(comm)
         MPI.Finalize()
         print(json.dumps({"rank": MPI.Comm_rank(comm), "provided": provided, "checks": NCHECK[0],

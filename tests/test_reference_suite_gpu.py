@@ -45,19 +45,20 @@ def test_reference_threads_device(n):
     assert len(summ) == n and all(s["nfail"] == 0 and s["provided"] == 3 for s in summ), summ
 
 
-@pytest.mark.parametrize("k", [1, 3])
-def test_concurrent_comms_beyond_residency(k):
-    """(~12 s) VERDICT r05 item 2: three communicators' 64 MiB Allreduce! at
+@pytest.mark.parametrize("k,mode", [(1, "stuck"), (3, "stuck"), (1, "stuck_so")])
+def test_concurrent_comms_beyond_residency(k, mode):
+    """(~18 s) VERDICT r05 item 2: three communicators' 64 MiB Allreduce! at
     once from three threads per rank, n = 3 on one GPU, no host gate (the
     one-rank-per-GPU protocol), grids at their residency caps, rank 0 first
     (tests/spmd/threads_worker.py stuck_case).  k = 1: the grids cannot all
     be resident, which waited forever in round 5; now every call of every
     rank ends with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS and stderr
     names MPIGX_CONCURRENT_COMMS.  k = 3 (the knob at the number of
-    communicators): exact."""
+    communicators): exact.  stuck_so: the same with stream-ordered launches
+    (8 MiB staged two-shot), cancelled by the process-wide watcher."""
     env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "3000", "MPIGX_CONCURRENT_COMMS": str(k),
            "MPIGX_MAX_BLOCKS": "4096", "MPIGX_SHARED_GATE": "0", "MPIGX_PEER_MEM": "xdev",
-           "THREADS_MODE": "stuck", "GPU_MAX_HW_QUEUES": "16"}
+           "THREADS_MODE": mode, "GPU_MAX_HW_QUEUES": "16"}
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "threads_worker.py"), 3, timeout=240, extra_env=env)
     msg = "\n".join(o[-3000:] for o in outs)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
