@@ -104,13 +104,14 @@ def stuck_case(comm, size, rank, stream_ordered=False):
     come back with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS (mpigx.cpp
     stuck_peer / the stall rule; stderr names the knob); with the knob at
     the number of communicators every result must be exact.
-    stream_ordered: the same with RCCL-style launches (8 MiB, the staged
-    two-shot, which needs no host exchange before its launch): the
-    process-wide watcher (mpigx.cpp watch_one) cancels, and the error comes
-    from mpigx_comm_synchronize."""
+    stream_ordered: the same with RCCL-style launches (the launcher sets
+    MPIGX_ZC_MIN=0: the staged two-shot, which needs no host exchange before
+    its launch, with grids at their caps): the process-wide watcher
+    (mpigx.cpp watch_one) cancels, and the error comes from
+    mpigx_comm_synchronize."""
     ncomm = 3
     comms = [MPI.Comm_dup(comm) for _ in range(ncomm)]
-    cnt = ((8 if stream_ordered else 64) << 20) // 4
+    cnt = (64 << 20) // 4
     xs = [torch.full((cnt,), float(rank + 1 + i), device="cuda") for i in range(ncomm)]
     ys = [torch.empty_like(x) for x in xs]
     want = [float(sum(q + 1 + i for q in range(size))) for i in range(ncomm)]

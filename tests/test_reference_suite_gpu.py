@@ -55,10 +55,12 @@ def test_concurrent_comms_beyond_residency(k, mode):
     rank ends with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS and stderr
     names MPIGX_CONCURRENT_COMMS.  k = 3 (the knob at the number of
     communicators): exact.  stuck_so: the same with stream-ordered launches
-    (8 MiB staged two-shot), cancelled by the process-wide watcher."""
+    (staged two-shot), cancelled by the process-wide watcher."""
     env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "3000", "MPIGX_CONCURRENT_COMMS": str(k),
            "MPIGX_MAX_BLOCKS": "4096", "MPIGX_SHARED_GATE": "0", "MPIGX_PEER_MEM": "xdev",
            "THREADS_MODE": mode, "GPU_MAX_HW_QUEUES": "16"}
+    if mode == "stuck_so":
+        env["MPIGX_ZC_MIN"] = "0"  # the staged two-shot: no host exchange before a stream-ordered launch
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "threads_worker.py"), 3, timeout=240, extra_env=env)
     msg = "\n".join(o[-3000:] for o in outs)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]

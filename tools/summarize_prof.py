@@ -59,7 +59,9 @@ def main(out, dest, tag):
     # the headline kernel, keyed for bench.py
     j = {"kernels": summary}
     for k in summary:
-        if "fold_local_kernel<mpigx::OpSum, float, 8, 0" in k or "fold_local_kernelINS_5OpSumEfLi8ELi0E" in k:
+        # the 256 MiB headline instantiation only (TREE, SH_FULL, U = 4): since
+        # round 6 smaller inputs launch the U = 1 / 2 instantiations
+        if "fold_local_kernel<mpigx::OpSum, float, 8, 0, 2, 4>" in k or "fold_local_kernelINS_5OpSumEfLi8ELi0ELi2ELi4E" in k:
             j["reduce_local_multi_f32_sum_8x256MiB"] = summary[k]["hbm_bytes_per_dispatch"]
     with open(os.path.join(dest, f"{tag}_traffic.json"), "w") as fh:
         json.dump(j, fh, indent=1)
