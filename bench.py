@@ -590,12 +590,31 @@ def bench_allreduce(args):
     # size sweep (mpigx), algorithm variants, the ring (MPIGX_ALGO=ring, one
     # ring / every coprime-stride ring) and the RCCL comparison point
     sweep, rccl = {}, {}
-    sizes = [8 << 10, 1 << 20, 16 << 20, 64 << 20, S, 1 << 30]
+    # config 3's sweep: every power of two from 8 KiB to 1 GiB,
+    # busbw and its fraction of the nominal aggregate xGMI ingress (distinct
+    # GPUs; null when the ranks share one GPU)
+    sizes = [(8 << 10) << k for k in range(18)]
+    if S not in sizes:
+        sizes.append(S)
+    peak_x = None if same_device else XGMI_LINK_GBPS * (n - 1)
+
+    def label(nb):
+        return f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"
+
     def sweep_section():
         for nb in sizes:
             tw, tk = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
-            sweep[f"{nb >> 10}KiB" if nb < (1 << 20) else f"{nb >> 20}MiB"] = {
-                "busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1), "ms": round(tw * 1e3, 4)}
+            sweep[label(nb)] = {"busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1),
+                                "algbw": round(nb / tw / 1e9, 1), "ms": round(tw * 1e3, 4),
+                                "frac_xgmi": round(busbw(nb, tk) / peak_x, 4) if peak_x else None}
+        # ring reduce-scatter + allgather against the default (config 3's
+        # "ring vs tree/direct"), 1 MiB .. 1 GiB
+        MPI.set_knob(comm, "ALGO", "ring")
+        for nb in [nb for nb in sizes if nb >= (1 << 20)]:
+            tw, tk = time_ar(nb, 5 if nb >= (256 << 20) else 10, 2)
+            sweep[f"ring_{label(nb)}"] = {"busbw": round(busbw(nb, tw), 1), "busbw_dev": round(busbw(nb, tk), 1),
+                                          "frac_xgmi": round(busbw(nb, tk) / peak_x, 4) if peak_x else None}
+        MPI.set_knob(comm, "ALGO", None)
         for nb in (1 << 20, 16 << 20):
             for algo in ("oneshot", "twoshot"):
                 MPI.set_knob(comm, "ALGO", algo)
