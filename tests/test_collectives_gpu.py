@@ -20,7 +20,7 @@ ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_MAX_BLOCKS"
 
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 8])
 def test_golden_collectives(n):
-    """(~35 s) Every MPICH-recorded golden collective case (tests/golden/mpich_golden.npz) reproduced bit for bit on device at n = 2..8."""
+    """(~36 s) Every MPICH-recorded golden collective case (tests/golden/mpich_golden.npz) reproduced bit for bit on device at n = 2..8."""
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "golden_worker.py"), n, timeout=900, extra_env=ENV)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     assert all(rc == 0 for rc in rcs), msg
@@ -31,7 +31,7 @@ def test_golden_collectives(n):
 
 @pytest.mark.parametrize("n", [2, 3, 5, 8])
 def test_golden_collectives_zero_copy(n):
-    """(~30 s) Every Allreduce through the zero-copy paths (pull: peers read the user
+    """(~28 s) Every Allreduce through the zero-copy paths (pull: peers read the user
     buffers through cached hipIpc registrations; push: ranks write into the
     peers' arenas and recvbufs); MPIGX_ZC_MIN=1 forces them at every size."""
     env = dict(ENV, MPIGX_ZC_MIN="1", MPIGX_ZC_REQUIRE="1")
@@ -54,7 +54,7 @@ def _summaries(outs):
 
 @pytest.mark.parametrize("n", [9, 10])
 def test_oracle_collectives_many_ranks(n):
-    """(~28 s) n = 9..15: pof2 = 8 with pre-step partners and n-1 > 8 peers to gather
+    """(~31 s) n = 9..15: pof2 = 8 with pre-step partners and n-1 > 8 peers to gather
     from (NMAX 16 kernels), staged and zero-copy paths, vs the oracle (MPICH
     recorded fixtures exist for n <= 8 only).  More than 10 rank processes on
     ONE GPU do not all get hardware queues at once (13 ranks: some ranks'

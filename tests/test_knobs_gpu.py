@@ -57,5 +57,5 @@ def test_zero_copy_import_failure_agreed():
 
 @pytest.mark.parametrize("base", [(1 << 31) - 12, (1 << 31) - 36])
 def test_ll_flag_generation_wrap(base):
-    """(~7 s) LL flags across the 2^31 epoch generation boundary (area cleared, no stale flag accepted)."""
+    """(~6 s) LL flags across the 2^31 epoch generation boundary (area cleared, no stale flag accepted)."""
     _run(2, "ll_wrap", MPIGX_EPOCH_BASE=str(base))

@@ -18,7 +18,7 @@ ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS"
 
 @pytest.mark.parametrize("n", [5, 8])
 def test_mpich_large_fixtures_on_device(n):
-    """(~10 s) MPICH-recorded 4,194,307 / 1,048,579-element collectives (mpich_large.npz) reproduced on device at n = 5, 8."""
+    """(~11 s) MPICH-recorded 4,194,307 / 1,048,579-element collectives (mpich_large.npz) reproduced on device at n = 5, 8."""
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "large_worker.py"), n, timeout=600, extra_env=ENV)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     assert all(rc == 0 for rc in rcs), msg

@@ -43,7 +43,7 @@ SLOW = pytest.mark.slow
                                              pytest.param("xdev", 2, "late_p2p", marks=SLOW),
                                              ("xdev", 2, "late_stream")])
 def test_late_rank_is_waited_for(cfg, n, scenario):
-    """(~35 s) A rank 2.5 x MPIGX_TIMEOUT_MS late — on its host, or on its
+    """(~32 s) A rank 2.5 x MPIGX_TIMEOUT_MS late — on its host, or on its
     GPU behind earlier stream work (late_stream) — is waited
     for: exact results, no error."""
     rcs, outs = launch(WORKER, n, timeout=240, extra_env=CONFIGS[cfg], args=(scenario,))

@@ -151,7 +151,7 @@ def test_reduce_local_matches_mpich_fixtures(L):
 
 
 def test_full_size_property(L):
-    """(~2 s) Config 2 at full size (8 x 256 MiB f32): SUM of (k+1)*ones in bf16-exact
+    """(~1 s) Config 2 at full size (8 x 256 MiB f32): SUM of (k+1)*ones in bf16-exact
     integers is exact, and linearity across two calls holds."""
     n, count = 8, 64 << 20
     ins = [torch.full((count,), float(k + 1), device="cuda") for k in range(n)]

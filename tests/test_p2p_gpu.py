@@ -31,7 +31,7 @@ def _records(outs):
 
 @pytest.mark.parametrize("n", [2, 3, 4])
 def test_p2p_scenarios_device_match_mpich(n):
-    """(~10 s) MPICH-recorded point-to-point scenarios reproduced on device at n = 2, 3, 4."""
+    """(~11 s) MPICH-recorded point-to-point scenarios reproduced on device at n = 2, 3, 4."""
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "p2p_worker.py"), n, timeout=600, extra_env=ENV)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     assert all(rc == 0 for rc in rcs), msg
@@ -48,7 +48,7 @@ def test_p2p_scenarios_device_match_mpich(n):
 
 @pytest.mark.parametrize("n,seed,maxb", [(2, 7, 8 << 20), (4, 11, 2 << 20), (3, 5, 1 << 16)])
 def test_p2p_random_traffic_device(n, seed, maxb):
-    """(~11 s) Random point-to-point traffic against the matching model (oracle/p2p_model.py)."""
+    """(~13 s) Random point-to-point traffic against the matching model (oracle/p2p_model.py)."""
     env = dict(ENV, P2P_SEED=str(seed), P2P_MAXB=str(maxb))
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "p2p_random_worker.py"), n, timeout=600, extra_env=env)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))

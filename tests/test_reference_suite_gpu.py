@@ -27,7 +27,7 @@ def test_reference_suite_device(n, cfg):
 
 @pytest.mark.parametrize("n", [2, 3])
 def test_reference_threads_device(n):
-    """(~10 s) test/test_threads.jl in device mode (tests/spmd/threads_worker.py):
+    """(~8 s) test/test_threads.jl in device mode (tests/spmd/threads_worker.py):
     Init_thread(THREAD_MULTIPLE), threaded Irecv! / Isend of one-element
     device views, Waitall on the main thread."""
     # the worker runs collectives of three communicators at once: their
@@ -47,7 +47,7 @@ def test_reference_threads_device(n):
 
 @pytest.mark.parametrize("k,mode", [(1, "stuck"), (3, "stuck"), (1, "stuck_so")])
 def test_concurrent_comms_beyond_residency(k, mode):
-    """(~18 s) VERDICT r05 item 2: three communicators' 64 MiB Allreduce! at
+    """(~16 s) VERDICT r05 item 2: three communicators' 64 MiB Allreduce! at
     once from three threads per rank, n = 3 on one GPU, no host gate (the
     one-rank-per-GPU protocol), grids at their residency caps, rank 0 first
     (tests/spmd/threads_worker.py stuck_case).  k = 1: the grids cannot all

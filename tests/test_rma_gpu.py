@@ -22,7 +22,7 @@ ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_MAX_BLOCKS"
 
 @pytest.mark.parametrize("n", [2, 3, 4])
 def test_rma_scenarios_device_match_mpich(n, tmp_path):
-    """(~12 s) test_onesided.jl / test_shared_win.jl restated and the Accumulate matrix: MPICH-recorded records reproduced at n = 2, 3, 4."""
+    """(~15 s) test_onesided.jl / test_shared_win.jl restated and the Accumulate matrix: MPICH-recorded records reproduced at n = 2, 3, 4."""
     env = dict(ENV, RMA_OUT=str(tmp_path / "rma"))
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "rma_worker.py"), n, timeout=600, extra_env=env)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))

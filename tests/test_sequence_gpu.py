@@ -20,7 +20,7 @@ ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_TIMEOUT_MS"
 
 @pytest.mark.parametrize("n,cfg", [(8, "same"), (8, "xdev")])
 def test_scan_exscan_reduce_sequence_fresh_comm(n, cfg):
-    """(~9 s) cfg xdev: the one-rank-per-GPU signalling, no host gate (the early
+    """(~8 s) cfg xdev: the one-rank-per-GPU signalling, no host gate (the early
     ranks' kernels wait on the device while their peers run torch work)."""
     env = dict(ENV, MPIGX_PEER_MEM="xdev", MPIGX_SHARED_GATE="0") if cfg == "xdev" else ENV
     rcs, outs = launch(os.path.join(ROOT, "tools", "scan_repro.py"), n, timeout=600, extra_env=env)

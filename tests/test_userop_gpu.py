@@ -25,7 +25,7 @@ ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_MAX_BLOCKS"
 @pytest.mark.parametrize("n", [2, 3, 4])
 @pytest.mark.parametrize("hostcb", ["0", "1", "libmpi"])
 def test_user_ops_device_match_mpich(n, hostcb, tmp_path):
-    """(~31 s) User ops (host-staged, device callback, libmpi MPI_Op_create) reproduce MPICH's results at n = 2, 3, 4."""
+    """(~29 s) User ops (host-staged, device callback, libmpi MPI_Op_create) reproduce MPICH's results at n = 2, 3, 4."""
     env = dict(ENV, UO_OUT=str(tmp_path / "uo"), USEROP_HOSTCB=hostcb)
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "userop_worker.py"), n, timeout=300, extra_env=env)
     recs = {}

@@ -64,7 +64,7 @@ def test_golden_collectives_xdev(n):
 
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_golden_collectives_zero_copy_xdev(n):
-    """(~22 s) The zero-copy paths (pull, push, pull-push, ring, zero-copy Reduce /
+    """(~23 s) The zero-copy paths (pull, push, pull-push, ring, zero-copy Reduce /
     Scan / Bcast relay) at every fixture size."""
     env = dict(GOLDEN_ENV, MPIGX_ZC_MIN="1", MPIGX_ZC_REQUIRE="1")
     rcs, res, msg = _run("golden_worker.py", n, env)
@@ -76,7 +76,7 @@ def test_golden_collectives_zero_copy_xdev(n):
 
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_headline_sizes_xdev(n):
-    """(~15 s) 256 MiB Allreduce (whole buffer), 512 MiB Bcast / Allgather /
+    """(~17 s) 256 MiB Allreduce (whole buffer), 512 MiB Bcast / Allgather /
     Alltoall, 64 Mi-element Scan / Exscan / Reduce, every algorithm at 16 MiB
     and 1 MiB, on the production grid."""
     rcs, res, msg = _run("headline_worker.py", n, dict(XDEV, MPIGX_HEADLINE_EXTRA="1"))
@@ -99,7 +99,7 @@ def test_mpich_large_fixtures_xdev():
 
 
 def test_zero_copy_views_xdev():
-    """(~4 s) Optimistic launches on cached views, a rank alone switching buffers
+    """(~3 s) Optimistic launches on cached views, a rank alone switching buffers
     (the abort verdict through the completion word), import agreement."""
     env = dict(XDEV, MPIGX_MAX_BLOCKS="16", MPIGX_STAGING_BYTES=str(64 << 20))
     rcs, res, msg = _run("zc_worker.py", 2, env, timeout=600)
@@ -111,7 +111,7 @@ def test_zero_copy_views_xdev():
 
 @pytest.mark.parametrize("worker", ["headline_worker.py", "golden_worker.py"])
 def test_production_grid_xdev(worker):
-    """(~10 s) Two ranks, the cross-GPU signalling AND the production grid: without
+    """(~9 s) Two ranks, the cross-GPU signalling AND the production grid: without
     the shared-GPU residency headroom (MPIGX_SHARE_HEADROOM=0) every
     collective kernel of a 2-rank communicator gets 256 blocks, as on a GPU of
     its own (bench r05p: pull / push / pull-push phases report 256 blocks),

@@ -17,7 +17,7 @@ ENV = {"MPIGX_DEVICE": "0", "MPIGX_INIT_TIMEOUT_MS": "60000", "MPIGX_MAX_BLOCKS"
 
 @pytest.mark.parametrize("n", [2, 4])
 def test_zero_copy_views(n):
-    """(~7 s) Optimistic launches on cached zero-copy views, re-registration after a buffer change, exact results."""
+    """(~8 s) Optimistic launches on cached zero-copy views, re-registration after a buffer change, exact results."""
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "zc_worker.py"), n, timeout=600, extra_env=ENV)
     msg = "\n".join(f"--- rank {r} rc={rc}\n{o[-3000:]}" for r, (rc, o) in enumerate(zip(rcs, outs)))
     assert all(rc == 0 for rc in rcs), msg
