@@ -93,6 +93,32 @@ def test_full_shape_multi_vector(L):
             assert same_bits(got, expected(ins, dtname, opname, 0), dtname == "BFLOAT16"), (dtname, opname, count)
 
 
+def test_local_u_variants(L):
+    """(~6 s) The 8-buffer shape at every vectors-per-thread variant the host
+    picks by size (common.hpp local_u, round 6): U = 1 / 2 / 4 forced through
+    MPIGX_LOCAL_U on ragged sizes with Rabenseifner boundaries inside
+    vectors, and the natural choice at sizes where it is 2 and 4 (f32: 2 Mi
+    and 4 Mi elements), bit-exact against the oracle."""
+    import os
+    try:
+        for u in ("1", "2", "4"):
+            os.environ["MPIGX_LOCAL_U"] = u
+            for dtname, opname in (("FLOAT", "SUM"), ("BFLOAT16", "SUM"), ("DOUBLE", "MAX"), ("INT64_T", "BXOR")):
+                for count in ((1 << 16) + 13, 3 * 1024 * 8 + 5):
+                    ins = make(dtname, opname, 8, count, 91 + count, edge=True)
+                    for order in (0, 1):  # MPICH tree / rank-ordered LINEAR
+                        got = run_multi(L, ins, dtname, opname, order)
+                        assert same_bits(got, expected(ins, dtname, opname, order), dtname == "BFLOAT16"), \
+                            (u, dtname, count, order)
+    finally:
+        os.environ.pop("MPIGX_LOCAL_U", None)
+    for dtname, opname, count in (("FLOAT", "SUM", (2 << 20) + 13), ("FLOAT", "MAX", (4 << 20) + 5),
+                                  ("DOUBLE", "SUM", (2 << 20) + 3), ("INT32_T", "BOR", (4 << 20) + 7)):
+        ins = make(dtname, opname, 8, count, 5 + count, edge=True)
+        got = run_multi(L, ins, dtname, opname, 0)
+        assert same_bits(got, expected(ins, dtname, opname, 0)), (dtname, opname, count)
+
+
 def test_bf16_random_bit_patterns(L):
     """(~1 s) bf16 definition (fp32 compute, RNE to bf16 after every op, NaN quiet) on
     uniformly random 16-bit patterns — NaN payloads, infinities, denormals,
