@@ -173,8 +173,10 @@ def vcoll_cases(comm, seed, ncases):
 
 def local_cases(seed, ncases):
     """The local MPI.Op kernel (config 2's API, mpigx_reduce_local_multi):
-    2-16 inputs, every valid (op, type), odd counts and unaligned buffers,
-    against the oracle's fold of the same inputs (an nin-rank Allreduce)."""
+    2-16 inputs, every valid (op, type), odd counts and unaligned buffers, and
+    config 2's aligned 8-input shape at sizes that draw every vectors-per-
+    thread variant, against the oracle's fold of the same inputs (an
+    nin-rank Allreduce)."""
     rng = np.random.default_rng(seed + 104729)
     fails, ran = [], 0
     stream = torch.cuda.current_stream()
@@ -183,12 +185,18 @@ def local_cases(seed, ncases):
         op = list(M.OPS)[rng.integers(len(M.OPS))]
         if M.op_valid(dt, op) != 0:
             continue
-        nin = int(rng.integers(2, 17))
+        # one case in three: config 2's shape — 8 aligned inputs (the SH_FULL
+        # vector kernel), at sizes up to 20 MiB per input so every
+        # vectors-per-thread variant the host picks by size (local_u: 1 / 2 /
+        # 4) is drawn; otherwise 2-16 inputs at element offsets
+        full = rng.integers(3) == 0
+        nin = 8 if full else int(rng.integers(2, 17))
         es = np.dtype(M.DTYPES[dt][1]).itemsize
-        count = int(rng.integers(1, (4 << 20) // es if rng.integers(3) == 0 else 5000))
+        top = (20 << 20) if full and rng.integers(2) == 0 else (4 << 20)
+        count = int(rng.integers(1, top // es if rng.integers(3) == 0 else 5000))
         ins = make(dt, op, nin, count, int(rng.integers(1 << 30)), edge=bool(rng.integers(3) == 0))
-        dins = [dev_at(x, int(rng.integers(3))) for x in ins]
-        out = dev_at(np.zeros_like(ins[0]), int(rng.integers(3)))
+        dins = [dev_at(x, 0 if full else int(rng.integers(3))) for x in ins]
+        out = dev_at(np.zeros_like(ins[0]), 0 if full else int(rng.integers(3)))
         arr = (ctypes.c_void_p * nin)(*[t.data_ptr() for t in dins])
         rc = MPI.lib().mpigx_reduce_local_multi(arr, nin, ctypes.c_void_p(out.data_ptr()), count, M.DTYPES[dt][0],
                                                 M.OPS[op], 0, ctypes.c_void_p(stream.cuda_stream))
