@@ -316,7 +316,11 @@ def bench_local(args):
                 "bf16_SUM_GBps": time_variant(torch.bfloat16, MPI.SUM),
                 "bf16_MAX_GBps": time_variant(torch.bfloat16, MPI.MAX)}
 
-    # message-size sweep of the same kernel (f32 SUM, 8 inputs), kernel time
+    # message-size sweep of the same kernel (f32 SUM, 8 inputs), HIP events
+    # over back-to-back launches: "us" issued through the Python mirror,
+    # "us_abi" through the raw C ABI, "us_graph" replayed from one captured
+    # HIP graph (device-bound: below ~4 MiB the eager loops measure the host
+    # issuing launches, not the kernel)
     sweep = {}
     for mib in (() if args.no_sweep else (1, 4, 16, 64)):
         k = mib << 18
@@ -332,6 +336,16 @@ def bench_local(args):
         e1.record(stream)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / reps * 1e3
+        # the same loop through the raw C ABI (what MPI.jl's ccall makes: no
+        # Python mirror between launches)
+        Lr, pin = MPI.lib(), (ctypes.c_void_p * len(xs))(*[x.data_ptr() for x in xs])
+        po, ps, fl, sm = ctypes.c_void_p(o.data_ptr()), ctypes.c_void_p(stream.cuda_stream), MPI.FLOAT.val, MPI.SUM.val
+        e0.record(stream)
+        for _ in range(reps):
+            Lr.mpigx_reduce_local_multi(pin, len(xs), po, k, fl, sm, 0, ps)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us_abi = e0.elapsed_time(e1) / reps * 1e3
         # the same launches replayed from one captured HIP graph: the host's
         # per-launch cost out of the loop (below ~4 MiB the eager loop above
         # is bound by the host issuing launches, not by the kernel)
@@ -348,6 +362,7 @@ def bench_local(args):
         usg = e0.elapsed_time(e1) / reps * 1e3
         del graph
         sweep[f"{mib}MiB"] = {"GBps": round((args.nbuf + 1) * k * 4 / (us / 1e6) / 1e9, 1), "us": round(us, 2),
+                              "us_abi": round(us_abi, 2),
                               "GBps_graph": round((args.nbuf + 1) * k * 4 / (usg / 1e6) / 1e9, 1),
                               "us_graph": round(usg, 2)}
     sweep[f"{args.mib}MiB"] = {"GBps": round(algo / (kern_ms / 1e3) / 1e9, 1), "us": round(kern_ms * 1e3, 2)}

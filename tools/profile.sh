@@ -17,4 +17,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv 
   python3 "$R/bench.py" --no-cpu-baseline --no-sweep --steps 5 --warmup 1 "$@" > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- \
   python3 "$R/bench.py" --no-cpu-baseline --no-sweep --steps 5 --warmup 1 "$@" > "$OUT/write.log" 2>&1
+# summaries into the box's profiles/ and beside the raw CSVs under
+# gpurun_out/ (the only part of a gpurun box's tree that comes back)
 python3 "$R/tools/summarize_prof.py" "$OUT" "$R/profiles" "$TAG"
+python3 "$R/tools/summarize_prof.py" "$OUT" "$OUT/summary" "$TAG" > /dev/null
