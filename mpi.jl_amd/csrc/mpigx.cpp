@@ -325,6 +325,7 @@ int shared_gate(mpigx_comm* c) {
 // finish()'s wait, plus stream-ordered communicators whose stream the watcher
 // last found busy.
 namespace {
+std::atomic<int> g_live_comms{0};     // communicators of this process (init .. release)
 std::atomic<int> g_busy_blocking{0};  // finish() waits in progress
 std::atomic<int> g_busy_streams{0};   // watched stream-ordered communicators with work queued
 struct BusyWait {
@@ -564,8 +565,10 @@ void note_launch(mpigx_comm* c, const PeerView& pv, unsigned grid) {
   } else {
     c->unflagged = true;
     // completion marker of a stream-ordered launch for the watcher (is this
-    // communicator busy: proc_busy / stuck_peer); ~1 us of host time
-    if (c->n > 1 && c->shm) {
+    // communicator busy: proc_busy / stuck_peer); ~1 us of host time, spent
+    // only while the process has another communicator (alone, this one can
+    // never make proc_busy reach 2)
+    if (c->n > 1 && c->shm && g_live_comms.load(std::memory_order_relaxed) >= 2) {
       if (!c->so_ev && hipEventCreateWithFlags(&c->so_ev, hipEventDisableTiming) != hipSuccess) {
         (void)hipGetLastError();
         c->so_ev = nullptr;
@@ -2435,6 +2438,7 @@ int knobs_from_env(mpigx_comm* c) {
 // allocations, the pinned page, peer mappings and the shm block.  Used by
 // mpigx_comm_free after its closing barrier and by every failed init.
 void comm_release(mpigx_comm* c) {
+  g_live_comms.fetch_sub(1, std::memory_order_relaxed);
   (void)hipSetDevice(c->device);
   if (c->stream || c->launch_seq) (void)hipStreamSynchronize(c->stream);
   watch_unregister(c);  // after the drain: a waiting stream-ordered launch needs the watcher to be cancelled
@@ -2747,6 +2751,7 @@ int mpigx_comm_init_rank(mpigx_comm_t* out, int nranks, const mpigx_unique_id_t*
   if (p.magic != kMagic) return MPIGX_ERR_ARG;
   HIPCK(hipSetDevice(device));
   mpigx_comm* c = new mpigx_comm();
+  g_live_comms.fetch_add(1, std::memory_order_relaxed);  // comm_release (every exit path) takes it back
   c->rank = rank;
   c->n = nranks;
   c->device = device;
