@@ -63,6 +63,14 @@ def test_concurrent_comms_beyond_residency(k, mode):
            "THREADS_MODE": mode, "GPU_MAX_HW_QUEUES": "16"}
     if mode == "stuck_so":
         env["MPIGX_ZC_MIN"] = "0"  # the staged two-shot: no host exchange before a stream-ordered launch
+    else:
+        # the pull-push two-shot with ticket-dealt slices ends in ONE
+        # whole-launch barrier (rank_barrier_grid): every block of every rank
+        # must be resident at once, so grids that cannot all fit deadlock for
+        # certain.  With per-block barriers only (the tuner's other choices)
+        # blocks pair by index and the residency headroom often lets them
+        # trickle through (r06h: k = 1 completed)
+        env.update(MPIGX_ALGO="pullpush", MPIGX_AR_SLICES="4")
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "threads_worker.py"), 3, timeout=240, extra_env=env)
     msg = "\n".join(o[-3000:] for o in outs)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
