@@ -364,8 +364,10 @@ def bench_local(args):
         sweep[f"{mib}MiB"] = {"GBps": round((args.nbuf + 1) * k * 4 / (us / 1e6) / 1e9, 1), "us": round(us, 2),
                               "us_abi": round(us_abi, 2),
                               "GBps_graph": round((args.nbuf + 1) * k * 4 / (usg / 1e6) / 1e9, 1),
-                              "us_graph": round(usg, 2)}
-    sweep[f"{args.mib}MiB"] = {"GBps": round(algo / (kern_ms / 1e3) / 1e9, 1), "us": round(kern_ms * 1e3, 2)}
+                              "us_graph": round(usg, 2),
+                              "frac_hbm_graph": round((args.nbuf + 1) * k * 4 / (usg / 1e6) / 1e9 / HBM_PEAK_GBPS, 4)}
+    sweep[f"{args.mib}MiB"] = {"GBps": round(algo / (kern_ms / 1e3) / 1e9, 1), "us": round(kern_ms * 1e3, 2),
+                               "frac_hbm": round(algo / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
     cpu_ar = None if args.no_cpu_baseline else cpu_reference_allreduce()
 
     traffic, traffic_src = traffic_from_profiles("reduce_local_multi_f32_sum_8x256MiB")
