@@ -809,6 +809,11 @@ def bench_allreduce(args):
                 cfg4[f"{nb >> 10}KiB"] = {
                     "bcast_busbw": round(nb / tb / 1e9, 2), "allgather_busbw": round(nb / tg / 1e9 * f, 2),
                     "alltoall_busbw": round(nb / ta / 1e9 * f, 2), "ok": bad == 0.0}
+                if peak_x:  # fraction of the nominal aggregate xGMI ingress (distinct GPUs)
+                    cfg4[f"{nb >> 10}KiB"].update(
+                        bcast_frac_xgmi=round(nb / tb / 1e9 / peak_x, 4),
+                        allgather_frac_xgmi=round(nb / tg / 1e9 * f / peak_x, 4),
+                        alltoall_frac_xgmi=round(nb / ta / 1e9 * f / peak_x, 4))
                 if tbs:
                     cfg4[f"{nb >> 10}KiB"]["bcast_sag_busbw"] = round(nb / tbs / 1e9, 2)
                 del buf, src, dst, a2s, a2r
