@@ -198,7 +198,9 @@ int mpigx_comm_set_reduce_order(mpigx_comm_t comm, int order);
                                         * collectives may run on a GPU at the same time (threads, or
                                         * stream-ordered launches on different streams); every spinning
                                         * kernel's grid is capped at 1/this of the device's resident blocks,
-                                        * so all of them fit at once (init-only) */
+                                        * so all of them fit at once (init-only); too low for the
+                                        * communicators in flight: the stuck call fails with
+                                        * MPI_ERR_OTHER after MPIGX_TIMEOUT_MS */
 #define MPIGX_KNOB_COUNT 21
 #define MPIGX_ALGO_AUTO 0     /* unset: static rules + the measured choices */
 #define MPIGX_ALGO_LL 1       /* "ll" */
@@ -226,9 +228,14 @@ int mpigx_comm_get_knob(mpigx_comm_t comm, int knob, long long *value);
  * cap is *cap x its resident blocks per CU). */
 int mpigx_comm_device_share(mpigx_comm_t comm, int *ranks, int *cap);
 
-/* How long a collective's blocks wait for a peer before the call fails with
- * MPI_ERR_OTHER and the communicator is marked broken (default
- * MPIGX_TIMEOUT_MS, 60000).  Local; applies to later calls.  ms >= 1. */
+/* The communicator's stall bound (default MPIGX_TIMEOUT_MS, 60000).  A call
+ * waits for a late peer as long as that peer's process lives; it fails with
+ * MPI_ERR_OTHER (the communicator marked broken) within about a second when
+ * a peer is gone or its communicator failed, and after this bound when
+ * every rank's GPU has sat in the same launch with none moving, or when a
+ * peer's launch, enqueued but never started, is stuck behind other
+ * communicators' kernels (MPIGX_CONCURRENT_COMMS).  Local; applies to later
+ * calls.  ms >= 1. */
 int mpigx_comm_set_timeout(mpigx_comm_t comm, long long ms);
 
 /* Diagnostics (phase stamps, signal-slot and mapping checks, tuner and
