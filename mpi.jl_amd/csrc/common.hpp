@@ -63,14 +63,15 @@ constexpr int local_u_max(int rep, int op, int shape) {
   return shape != SH_FULL ? 1 : (rep == R_BF16 && (op == O_MIN || op == O_MAX)) ? 1 : 4;
 }
 // ... and by size: at U = 4 a 1 MiB input made 64
-// blocks of 256 threads, a quarter of the CUs.  U halves until the one-pass
-// grid has at least kLocalMinBlocks blocks (or U is 1): U = 4 from 1 Mi
-// 16-B vectors per input (16 MiB), 2 from 512 Ki, 1 below.
-constexpr long long kLocalMinBlocks = 1024;
+// blocks of 256 threads, a quarter of the CUs.  Measured (graph-replayed
+// launches, profiles/r06b_local_u_sweep.json, r06m_local_variant_u.json):
+// U = 4 is fastest (or tied) from 4 MiB of f32 per input up — 256 blocks,
+// one per CU — and U = 1 below (1 MiB: 2.3 vs 4.5 us); U = 2 was never the
+// fastest at any size or for any (type, op).  So U = 4 from 256 Ki 16-B
+// vectors per input, 1 below.
+constexpr long long kLocalU4MinVec = 4ll * kThreads * 256;
 constexpr int local_u(int rep, int op, int shape, long long nvec) {
-  int u = local_u_max(rep, op, shape);
-  while (u > 1 && nvec < (long long)u * kThreads * kLocalMinBlocks) u /= 2;
-  return u;
+  return (local_u_max(rep, op, shape) >= 4 && nvec >= kLocalU4MinVec) ? 4 : 1;
 }
 
 // Fold schedule (template parameter of the fold kernels).

@@ -186,9 +186,9 @@ def local_cases(seed, ncases):
         if M.op_valid(dt, op) != 0:
             continue
         # one case in three: config 2's shape — 8 aligned inputs (the SH_FULL
-        # vector kernel), at sizes up to 20 MiB per input so every
-        # vectors-per-thread variant the host picks by size (local_u: 1 / 2 /
-        # 4) is drawn; otherwise 2-16 inputs at element offsets
+        # vector kernel), at sizes up to 20 MiB per input so both
+        # vectors-per-thread variants the host picks by size (local_u: 1 / 4)
+        # are drawn; otherwise 2-16 inputs at element offsets
         full = rng.integers(3) == 0
         nin = 8 if full else int(rng.integers(2, 17))
         es = np.dtype(M.DTYPES[dt][1]).itemsize

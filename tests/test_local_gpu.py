@@ -94,11 +94,12 @@ def test_full_shape_multi_vector(L):
 
 
 def test_local_u_variants(L):
-    """(~6 s) The 8-buffer shape at every vectors-per-thread variant the host
-    picks by size (common.hpp local_u, round 6): U = 1 / 2 / 4 forced through
+    """(~6 s) The 8-buffer shape at every vectors-per-thread variant
+    (common.hpp local_u, round 6): U = 1 / 2 / 4 forced through
     MPIGX_LOCAL_U on ragged sizes with Rabenseifner boundaries inside
-    vectors, and the natural choice at sizes where it is 2 and 4 (f32: 2 Mi
-    and 4 Mi elements), bit-exact against the oracle."""
+    vectors, and the host's own choice on both sides of its threshold (f32:
+    U = 1 below 1 Mi elements per input, 4 from there), bit-exact against
+    the oracle."""
     import os
     try:
         for u in ("1", "2", "4"):
@@ -112,8 +113,8 @@ def test_local_u_variants(L):
                             (u, dtname, count, order)
     finally:
         os.environ.pop("MPIGX_LOCAL_U", None)
-    for dtname, opname, count in (("FLOAT", "SUM", (2 << 20) + 13), ("FLOAT", "MAX", (4 << 20) + 5),
-                                  ("DOUBLE", "SUM", (2 << 20) + 3), ("INT32_T", "BOR", (4 << 20) + 7)):
+    for dtname, opname, count in (("FLOAT", "SUM", (1 << 20) - 13), ("FLOAT", "MAX", (1 << 20) + 5),
+                                  ("DOUBLE", "SUM", (1 << 19) + 3), ("INT32_T", "BOR", (4 << 20) + 7)):
         ins = make(dtname, opname, 8, count, 5 + count, edge=True)
         got = run_multi(L, ins, dtname, opname, 0)
         assert same_bits(got, expected(ins, dtname, opname, 0)), (dtname, opname, count)
