@@ -56,11 +56,13 @@ def main():
                     MPI.reduce_local_multi(xs, o, MPI.SUM)
             graph.replay()
             torch.cuda.synchronize()
-            a.record(s)
-            graph.replay()
-            b.record(s)
-            torch.cuda.synchronize()
-            usg = a.elapsed_time(b) / reps * 1e3
+            usg = 1e9
+            for _ in range(3):  # best of three replays (a single replay catches box noise)
+                a.record(s)
+                graph.replay()
+                b.record(s)
+                torch.cuda.synchronize()
+                usg = min(usg, a.elapsed_time(b) / reps * 1e3)
             row[f"{mib}MiB"] = {"us": round(us, 2), "GBps": round((nbuf + 1) * k * 4 / (us / 1e6) / 1e9, 1),
                                 "us_graph": round(usg, 2),
                                 "GBps_graph": round((nbuf + 1) * k * 4 / (usg / 1e6) / 1e9, 1)}
