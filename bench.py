@@ -312,9 +312,31 @@ def bench_local(args):
         ms = e0.elapsed_time(e1) / 5
         return round((args.nbuf + 1) * count * xs[0].element_size() / (ms / 1e3) / 1e9, 1)
 
+    def time_in_place(k):
+        """f32 SUM written over rank buffer k (out aliases input k: MPI_Reduce
+        / Allreduce IN_PLACE, MPI_Reduce_local's inoutbuf), on a copy of that
+        input: the same 9 x 256 MiB of traffic with one stream fewer, the
+        store landing in a DRAM row the thread has just read
+        (tools/mix_tune.hip)."""
+        xs = list(ins)
+        xs[k] = ins[k].clone()
+        for _ in range(2):
+            MPI.reduce_local_multi(xs, xs[k], MPI.SUM, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(5):
+            MPI.reduce_local_multi(xs, xs[k], MPI.SUM, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 5
+        del xs
+        return round((args.nbuf + 1) * count * 4 / (ms / 1e3) / 1e9, 1)
+
     variants = {"f32_MAX_GBps": time_variant(torch.float32, MPI.MAX),
                 "bf16_SUM_GBps": time_variant(torch.bfloat16, MPI.SUM),
-                "bf16_MAX_GBps": time_variant(torch.bfloat16, MPI.MAX)}
+                "bf16_MAX_GBps": time_variant(torch.bfloat16, MPI.MAX),
+                "f32_SUM_in_place_rank0_GBps": time_in_place(0),
+                f"f32_SUM_in_place_rank{args.nbuf - 1}_GBps": time_in_place(args.nbuf - 1)}
 
     # message-size sweep of the same kernel (f32 SUM, 8 inputs), HIP events
     # over back-to-back launches: "us" issued through the Python mirror,
