@@ -120,6 +120,30 @@ def test_local_u_variants(L):
         assert same_bits(got, expected(ins, dtname, opname, 0)), (dtname, opname, count)
 
 
+def test_output_aliases_an_input(L):
+    """(~2 s) The output written over one of the inputs (MPI_Reduce_local's
+    inoutbuf; the in-place variants bench.py reports): every leaf of an
+    element is loaded before its result is stored, so the result equals the
+    out-of-place fold bit for bit — at both vectors-per-thread choices, with
+    ragged tails and Rabenseifner boundaries inside vectors, tree and linear
+    order."""
+    for dtname, opname, count in (("FLOAT", "SUM", (1 << 20) + 13), ("FLOAT", "MAX", 3 * 1024 * 8 + 5),
+                                  ("BFLOAT16", "SUM", (4 << 20) + 3), ("INT64_T", "BXOR", (1 << 19) + 7)):
+        ins = make(dtname, opname, 8, count, 17 + count, edge=True)
+        h = M.DTYPES[dtname][0]
+        for order in (0, 1):
+            for k in (0, 7):
+                dins = [dev(x) for x in ins]
+                ptrs = (ctypes.c_void_p * 8)(*[t.data_ptr() for t in dins])
+                rc = L.mpigx_reduce_local_multi(ptrs, 8, ctypes.c_void_p(dins[k].data_ptr()), count, h, M.OPS[opname],
+                                                order, None)
+                assert rc == 0
+                torch.cuda.synchronize()
+                got = host(dins[k], ins[0], count)
+                assert same_bits(got, expected(ins, dtname, opname, order), dtname == "BFLOAT16"), \
+                    (dtname, opname, count, order, k)
+
+
 def test_bf16_random_bit_patterns(L):
     """(~1 s) bf16 definition (fp32 compute, RNE to bf16 after every op, NaN quiet) on
     uniformly random 16-bit patterns — NaN payloads, infinities, denormals,
