@@ -64,6 +64,38 @@ __global__ __launch_bounds__(256) void mix(P a) {
   if (!STORE && acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u) a.sink[threadIdx.x] = acc;
 }
 
+// the same 8 : 1 stream with the inputs read one after another inside each
+// thread (G inputs at a time, a vmcnt(0) wait between groups): the blocks of
+// one dispatch wave start together, so across the GPU only G input streams
+// (+ the output) are active at once instead of 8
+template <int G>
+__global__ __launch_bounds__(256) void mix_seq(P a) {
+  constexpr int U = 4;
+  const long long base = (long long)blockIdx.x * (U * 256) + threadIdx.x;
+  u32x4 acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = u32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int k0 = 0; k0 < 8; k0 += G) {
+    u32x4 x[U][G];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < G; ++k) x[u][k] = __builtin_nontemporal_load(a.in[k0 + k] + base + u * 256);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < G; ++k) acc[u] ^= x[u][k];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.out + (base - threadIdx.x), 0, U * 256 * 16,
+                                                                  0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(acc[u], rs, (int)(threadIdx.x + u * 256) * 16, 0, 16);
+  }
+}
+
 int main(int argc, char** argv) {
   const int R = argc > 1 ? atoi(argv[1]) : 7;
   const long long S = 256ll << 20;
@@ -96,6 +128,9 @@ int main(int argc, char** argv) {
       {"4R:1W separate out", 5.0 * S, [&] { hipLaunchKernelGGL((mix<4, true>), G, B, 0, 0, p); }},
       {"2R:1W separate out", 3.0 * S, [&] { hipLaunchKernelGGL((mix<2, true>), G, B, 0, 0, p); }},
       {"1R:1W copy", 2.0 * S, [&] { hipLaunchKernelGGL((mix<1, true>), G, B, 0, 0, p); }},
+      {"8R:1W inputs one at a time", 9.0 * S, [&] { hipLaunchKernelGGL((mix_seq<1>), G, B, 0, 0, p); }},
+      {"8R:1W inputs two at a time", 9.0 * S, [&] { hipLaunchKernelGGL((mix_seq<2>), G, B, 0, 0, p); }},
+      {"8R:1W inputs four at a time", 9.0 * S, [&] { hipLaunchKernelGGL((mix_seq<4>), G, B, 0, 0, p); }},
       {"8R read only", 8.0 * S, [&] { hipLaunchKernelGGL((mix<8, false>), G, B, 0, 0, p); }},
       {"1R read only", 1.0 * S, [&] { hipLaunchKernelGGL((mix<1, false>), G, B, 0, 0, p); }},
   };
