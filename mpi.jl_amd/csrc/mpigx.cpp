@@ -377,8 +377,9 @@ void note_stuck(mpigx_comm* c, int who, double t, const double* since) {
 // GPU has sat in past the timeout (stuck_peer; checked every 0.25 s).  The
 // cancelled kernels record a timeout in the error word, which the next
 // synchronizing call reports (mpigx_comm_synchronize / any blocking call),
-// breaking the communicator.  Unlike a blocking call there is no
-// every-rank-in-the-launch stall rule: a stream-ordered launch that never
+// breaking the communicator.  The every-rank-in-the-launch stall rule
+// applies only while other communicators' collectives are in flight (the
+// partial-residency deadlock); otherwise a stream-ordered launch that never
 // completes for a protocol reason hangs, as an RCCL kernel would.
 // One thread for the process however many communicators there are (an
 // application with hundreds of Comm_split results must not get hundreds of
@@ -422,6 +423,26 @@ void watch_one(mpigx_comm* c, bool check) {
     if (who >= 0) {
       note_stuck(c, who, t, c->wstuck_since);
       why = "stuck behind other communicators' kernels";
+    } else if (me.kseq_enq.load(std::memory_order_relaxed) == st) {
+      // partial residency: launch st is the last this rank enqueued (so my
+      // stream holds no later work I could be late with), every rank's GPU
+      // is in it, none has left it for the timeout, and other
+      // communicators' collectives run somewhere — their grids hold the
+      // slots this launch's missing blocks need.  Without other
+      // communicators in flight a stream-ordered launch keeps RCCL's rule
+      // and waits.
+      bool all_in = true, others = busy_comms() >= 2;
+      for (int q = 0; q < c->n; ++q) {
+        if (q == c->rank) continue;
+        all_in &= c->shm->ranks[q].kseq_run.load(std::memory_order_acquire) == st;
+        others |= c->shm->ranks[q].proc_busy.load(std::memory_order_relaxed) >= 2;
+      }
+      if (all_in && others) {
+        who = c->rank;
+        why = "every rank's GPU is in this launch and none has left it while other communicators' collectives "
+              "run (their grids do not fit on the GPU together: set MPIGX_CONCURRENT_COMMS to the number of "
+              "communicators in flight at once)";
+      }
     }
   }
   if (why) {

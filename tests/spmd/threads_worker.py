@@ -104,11 +104,9 @@ def stuck_case(comm, size, rank, stream_ordered=False):
     come back with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS (mpigx.cpp
     stuck_peer / the stall rule; stderr names the knob); with the knob at
     the number of communicators every result must be exact.
-    stream_ordered: the same with RCCL-style launches (the launcher sets
-    MPIGX_ZC_MIN=0: the staged two-shot, which needs no host exchange before
-    its launch, with grids at their caps): the process-wide watcher
-    (mpigx.cpp watch_one) cancels, and the error comes from
-    mpigx_comm_synchronize."""
+    stream_ordered: the same with RCCL-style launches: the process-wide
+    watcher (mpigx.cpp watch_one) cancels a stuck or partially resident
+    launch, and the error comes from mpigx_comm_synchronize."""
     ncomm = 3
     comms = [MPI.Comm_dup(comm) for _ in range(ncomm)]
     cnt = (64 << 20) // 4

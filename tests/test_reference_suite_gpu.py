@@ -54,23 +54,22 @@ def test_concurrent_comms_beyond_residency(k, mode):
     be resident, which waited forever in round 5; now every call of every
     rank ends with MPI_ERR_OTHER within about MPIGX_TIMEOUT_MS and stderr
     names MPIGX_CONCURRENT_COMMS.  k = 3 (the knob at the number of
-    communicators): exact.  stuck_so: three communicators' stream-ordered
-    launches at once (staged two-shot) with k = 1: they make progress, and the
-    process-wide watcher must not take them for stuck (or, should one stall,
-    it ends with the named MPI_ERR_OTHER)."""
+    communicators): exact.  stuck_so: the same three communicators with
+    stream-ordered launches at k = 1 (the ranks launch together after each
+    zero-copy view agreement): every thread comes back, exact or with the
+    named MPI_ERR_OTHER from the process-wide watcher."""
     env = {"MPIGX_DEVICE": "0", "MPIGX_TIMEOUT_MS": "3000", "MPIGX_CONCURRENT_COMMS": str(k),
            "MPIGX_MAX_BLOCKS": "4096", "MPIGX_SHARED_GATE": "0", "MPIGX_PEER_MEM": "xdev",
            "THREADS_MODE": mode, "GPU_MAX_HW_QUEUES": "16"}
-    if mode == "stuck_so":
-        env["MPIGX_ZC_MIN"] = "0"  # the staged two-shot: no host exchange before a stream-ordered launch
-    else:
-        # the pull-push two-shot with ticket-dealt slices ends in ONE
-        # whole-launch barrier (rank_barrier_grid): every block of every rank
-        # must be resident at once, so grids that cannot all fit deadlock for
-        # certain.  With per-block barriers only (the tuner's other choices)
-        # blocks pair by index and the residency headroom often lets them
-        # trickle through (r06h: k = 1 completed)
-        env.update(MPIGX_ALGO="pullpush", MPIGX_AR_SLICES="4")
+    # the pull-push two-shot with ticket-dealt slices ends in ONE whole-launch
+    # barrier (rank_barrier_grid): every block of every rank must be resident
+    # at once, so grids that cannot all fit deadlock for certain when rank 0's
+    # are resident first (blocking mode).  With per-block barriers only (the
+    # tuner's other choices) blocks pair by index and the residency headroom
+    # often lets them trickle through (r06h: k = 1 completed).  Stream-ordered,
+    # the zero-copy view is agreed on the host before each launch, so the
+    # ranks launch together and which grids win the slots is up to the GPU
+    env.update(MPIGX_ALGO="pullpush", MPIGX_AR_SLICES="4")
     rcs, outs = launch(os.path.join(ROOT, "tests", "spmd", "threads_worker.py"), 3, timeout=240, extra_env=env)
     msg = "\n".join(o[-3000:] for o in outs)
     summ = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{") and '"checks"' in l]
@@ -79,11 +78,9 @@ def test_concurrent_comms_beyond_residency(k, mode):
     assert len(summ) == 3 and all(s["nfail"] == 0 for s in summ), summ
     assert len(stuck) == 3, msg
     if mode == "stuck_so":
-        # the staged two-shot's barriers pair block b with the peers' block
-        # b, and the residency headroom leaves a slot per CU free, so these
-        # launches make progress (r06d/r06e: all exact): what this case
-        # checks is that the watcher's stuck rule does not fire on them, or
-        # that, should a stall happen, it is the named MPI_ERR_OTHER
+        # every thread comes back: exact, or the named MPI_ERR_OTHER from the
+        # process-wide watcher (stuck peer, or every rank in a launch that
+        # other communicators' grids keep from completing)
         assert all(r is True or r == "MPIError 15" for s in stuck for r in s["stuck_results"]), stuck
         if any(s["errors"] for s in stuck):
             assert "MPIGX_CONCURRENT_COMMS" in msg, msg
