@@ -714,6 +714,7 @@ int finish(mpigx_comm* c) {
               bool others = busy_comms() >= 2;
               for (int q = 0; q < c->n && !others; ++q)
                 others = c->shm->ranks[q].proc_busy.load(std::memory_order_relaxed) >= 2;
+              who = c->rank;  // (the message names no peer: every rank is in the launch)
               why = others ? "every rank's GPU is in this launch and none has moved while other communicators' "
                              "collectives run (their grids do not fit on the GPU together: set "
                              "MPIGX_CONCURRENT_COMMS to the number of communicators in flight at once)"
