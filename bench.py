@@ -261,9 +261,21 @@ def bench_local(args):
         torch.cuda.synchronize()
         return a.elapsed_time(b) / reps
 
+    # everything beside the headline is guarded: a section that raises is
+    # recorded in `errors` and the headline line is still printed
+    errors = {}
+
+    def guarded(name, fn, default=None):
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001
+            errors[name] = f"{type(e).__name__}: {str(e)[:200]}"
+            torch.cuda.synchronize()
+            return default
+
     probes = len(ins) in (1, 2, 4, 8)
-    read_ms = [read_probe_ms()] if probes else []
-    mix_ms = [mix_probe_ms()] if probes else []
+    read_ms = guarded("read_probe", lambda: [read_probe_ms()], []) if probes else []
+    mix_ms = guarded("mix_probe", lambda: [mix_probe_ms()], []) if probes else []
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -281,8 +293,9 @@ def bench_local(args):
     kern_ms = e0.elapsed_time(e1) / args.steps
     algo = (args.nbuf + 1) * S
     if read_ms:
-        read_ms.append(read_probe_ms())
-        mix_ms.append(mix_probe_ms())
+        read_ms += guarded("read_probe", lambda: [read_probe_ms()], [])
+    if mix_ms:
+        mix_ms += guarded("mix_probe", lambda: [mix_probe_ms()], [])
 
     # parity spot check (the probes above wrote `out`: one more fold first)
     step()
@@ -332,11 +345,12 @@ def bench_local(args):
         del xs
         return round((args.nbuf + 1) * count * 4 / (ms / 1e3) / 1e9, 1)
 
-    variants = {"f32_MAX_GBps": time_variant(torch.float32, MPI.MAX),
-                "bf16_SUM_GBps": time_variant(torch.bfloat16, MPI.SUM),
-                "bf16_MAX_GBps": time_variant(torch.bfloat16, MPI.MAX),
-                "f32_SUM_in_place_rank0_GBps": time_in_place(0),
-                f"f32_SUM_in_place_rank{args.nbuf - 1}_GBps": time_in_place(args.nbuf - 1)}
+    variants = guarded("variants", lambda: {
+        "f32_MAX_GBps": time_variant(torch.float32, MPI.MAX),
+        "bf16_SUM_GBps": time_variant(torch.bfloat16, MPI.SUM),
+        "bf16_MAX_GBps": time_variant(torch.bfloat16, MPI.MAX),
+        "f32_SUM_in_place_rank0_GBps": time_in_place(0),
+        f"f32_SUM_in_place_rank{args.nbuf - 1}_GBps": time_in_place(args.nbuf - 1)}, {})
 
     # message-size sweep of the same kernel (f32 SUM, 8 inputs), HIP events
     # over back-to-back launches: "us" issued through the Python mirror,
@@ -344,7 +358,7 @@ def bench_local(args):
     # HIP graph (device-bound: below ~4 MiB the eager loops measure the host
     # issuing launches, not the kernel)
     sweep = {}
-    for mib in (() if args.no_sweep else (1, 4, 16, 64)):
+    def sweep_point(mib):
         k = mib << 18
         xs = [x[:k] for x in ins]
         o = out[:k]
@@ -390,6 +404,9 @@ def bench_local(args):
                               "GBps_graph": round((args.nbuf + 1) * k * 4 / (usg / 1e6) / 1e9, 1),
                               "us_graph": round(usg, 2),
                               "frac_hbm_graph": round((args.nbuf + 1) * k * 4 / (usg / 1e6) / 1e9 / HBM_PEAK_GBPS, 4)}
+
+    for mib in (() if args.no_sweep else (1, 4, 16, 64)):
+        guarded(f"sweep_{mib}MiB", lambda: sweep_point(mib))
     sweep[f"{args.mib}MiB"] = {"GBps": round(algo / (kern_ms / 1e3) / 1e9, 1), "us": round(kern_ms * 1e3, 2),
                                "frac_hbm": round(algo / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
     cpu_ar = None if args.no_cpu_baseline else cpu_reference_allreduce()
@@ -398,7 +415,8 @@ def bench_local(args):
     print(json.dumps(build_local_line({
         "nbuf": args.nbuf, "mib": args.mib, "steps": args.steps, "warmup": args.warmup, "wall_s": wall,
         "kern_ms": kern_ms, "read_ms": read_ms, "mix_ms": mix_ms, "parity": parity, "variants": variants,
-        "sweep": sweep, "cpu": cpu, "cpu_ar": cpu_ar, "traffic": traffic, "traffic_src": traffic_src})), flush=True)
+        "sweep": sweep, "cpu": cpu, "cpu_ar": cpu_ar, "traffic": traffic, "traffic_src": traffic_src,
+        "errors": errors})), flush=True)
 
 
 def build_local_line(m):
@@ -446,6 +464,7 @@ def build_local_line(m):
         "variants": m["variants"],
         "sweep_local_f32_sum": m["sweep"],
         "cpu_reference_allreduce_256MiB": m["cpu_ar"],
+        "errors": m.get("errors") or None,
     }
 
 
